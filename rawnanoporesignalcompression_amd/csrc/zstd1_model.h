@@ -1,0 +1,360 @@
+// zstd1_model.h -- serial composition of zstd1_common.h into a full `ZSTD_compress(.., 1)` for one
+// source of at most 128 KiB (single block), and a spec (RFC 8878) frame decoder.
+//
+// Host and device: the GPU kernels run the serial parts of these on one lane; the host build
+// (libpgn_model.so, test-only) lets the test-suite fuzz the exact same code against libzstd.
+#pragma once
+#include "zstd1_common.h"
+
+namespace pgn {
+namespace z1 {
+
+// ---------------------------------------------------------------------------------------------
+// ZSTD_compressBlock_fast (libzstd 1.4.x, two positions per step, kSearchStrength 8, stepSize 2),
+// fresh context: window base = src - 1 (prefixStartIndex 1), hash table zeroed, reps {1, 4, 8}
+// with offset_2 invalidated at the first position.  Positions below are offsets into src; table
+// entries hold indices (= offset + 1).  Appends sequences; literals are implied by the sequences
+// (the literal bytes are src[anchor .. anchor+litLength)).  Returns nbSeq; *lastLL = trailing
+// literal run.
+// ---------------------------------------------------------------------------------------------
+PGN_HD size_t match_count(const uint8_t* src, size_t a, size_t b, size_t end)
+{
+    size_t n = 0;
+    while (a + n < end && src[a + n] == src[b + n]) n++;
+    return n;
+}
+
+PGN_HD size_t fast_search_serial(const uint8_t* src, size_t n, const Params& p, uint32_t* ht, Seq* seqs,
+                                 size_t* lastLL)
+{
+    const unsigned hlog = p.hashLog, mls = p.mls;
+    for (size_t i = 0; i < ((size_t)1 << hlog); i++) ht[i] = 0;
+    size_t nbSeq = 0;
+    long ip0 = 1, ip1 = 2, anchor = 0;
+    const long iend = (long)n, ilimit = (long)n - 8;
+    uint32_t offset_1 = 1, offset_2 = 0;  // offset_2 (4) > maxRep (1): invalidated
+    while (ip1 < ilimit) {
+        long ip2 = ip0 + 2;
+        uint32_t h0 = hash_at(src + ip0, hlog, mls);
+        uint32_t h1 = hash_at(src + ip1, hlog, mls);
+        uint32_t val0 = rd32(src + ip0), val1 = rd32(src + ip1);
+        uint32_t cur0 = (uint32_t)ip0 + 1, cur1 = (uint32_t)ip1 + 1;
+        uint32_t mi0 = ht[h0], mi1 = ht[h1];
+        ht[h0] = cur0;
+        ht[h1] = cur1;
+        long match0;
+        size_t mLength;
+        uint32_t offcode;
+        if ((offset_1 > 0) && (rd32(src + ip2 - offset_1) == rd32(src + ip2))) {
+            mLength = (src[ip2 - 1] == src[ip2 - (long)offset_1 - 1]) ? 1 : 0;
+            ip0 = ip2 - (long)mLength;
+            match0 = ip0 - (long)offset_1;
+            mLength += 4;
+            offcode = 0;
+        } else {
+            bool found = false;
+            if ((mi0 > 1) && rd32(src + mi0 - 1) == val0) {
+                match0 = (long)mi0 - 1;
+                found = true;
+            } else if ((mi1 > 1) && rd32(src + mi1 - 1) == val1) {
+                ip0 = ip1;
+                match0 = (long)mi1 - 1;
+                found = true;
+            }
+            if (!found) {
+                long step = ((ip0 - anchor) >> 7) + 2;
+                ip0 += step;
+                ip1 += step;
+                continue;
+            }
+            offset_2 = offset_1;
+            offset_1 = (uint32_t)(ip0 - match0);
+            offcode = offset_1 + 2;
+            mLength = 4;
+            while ((ip0 > anchor) && (match0 > 0) && (src[ip0 - 1] == src[match0 - 1])) {
+                ip0--;
+                match0--;
+                mLength++;
+            }
+        }
+        mLength += match_count(src, (size_t)ip0 + mLength, (size_t)match0 + mLength, (size_t)iend);
+        seqs[nbSeq].litLength = (uint32_t)(ip0 - anchor);
+        seqs[nbSeq].offset = offcode + 1;
+        seqs[nbSeq].mlBase = (uint32_t)(mLength - 3);
+        nbSeq++;
+        ip0 += (long)mLength;
+        anchor = ip0;
+        if (ip0 <= ilimit) {
+            ht[hash_at(src + cur0 + 1, hlog, mls)] = cur0 + 2;
+            ht[hash_at(src + ip0 - 2, hlog, mls)] = (uint32_t)(ip0 - 2) + 1;
+            if (offset_2 > 0) {
+                while ((ip0 <= ilimit) && (rd32(src + ip0) == rd32(src + ip0 - offset_2))) {
+                    size_t rLength = match_count(src, (size_t)ip0 + 4, (size_t)ip0 + 4 - offset_2, (size_t)iend) + 4;
+                    uint32_t t = offset_2; offset_2 = offset_1; offset_1 = t;
+                    ht[hash_at(src + ip0, hlog, mls)] = (uint32_t)ip0 + 1;
+                    ip0 += (long)rLength;
+                    seqs[nbSeq].litLength = 0;
+                    seqs[nbSeq].offset = 1;
+                    seqs[nbSeq].mlBase = (uint32_t)(rLength - 3);
+                    nbSeq++;
+                    anchor = ip0;
+                }
+            }
+        }
+        ip1 = ip0 + 1;
+    }
+    *lastLL = (size_t)(iend - anchor);
+    return nbSeq;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Literals section (ZSTD_compressLiterals -> HUF_compress{1,4}X_repeat with a fresh table).
+// `work` must hold a LitWork.  Returns section size written at dst.
+// ---------------------------------------------------------------------------------------------
+struct LitWork {
+    uint32_t count[256];
+    HufNode nodes[2 * 256 + 1];
+    uint8_t nbBits[256];
+    uint16_t val[256];
+    FseCTable fct;
+    uint8_t scratch[64];
+};
+
+PGN_HD size_t write_raw_literals(uint8_t* dst, const uint8_t* lit, size_t n)
+{
+    size_t fl = write_rawrle_lit_header(dst, n, kSetBasic);
+    for (size_t i = 0; i < n; i++) dst[fl + i] = lit[i];
+    return fl + n;
+}
+
+// Huffman-encode `n` symbols (1X stream) into dst; returns bytes (end mark included).
+PGN_HD size_t huf_encode_1x(uint8_t* dst, const uint8_t* src, size_t n, const uint8_t* nbBits, const uint16_t* val)
+{
+    BitW bw;
+    bw_init(bw, dst);
+    for (size_t i = n; i-- > 0;) bw_add(bw, val[src[i]], nbBits[src[i]]);
+    return bw_close(bw, dst);
+}
+
+PGN_HD size_t compress_literals(uint8_t* dst, const uint8_t* lit, size_t n, LitWork& w)
+{
+    if (n <= 63) return write_raw_literals(dst, lit, n);
+    const size_t minGain = (n >> 6) + 2;
+    const size_t lhSize = huf_lit_header_size(n);
+    const bool singleStream = n < 256;
+    // HIST_count_wksp
+    for (int s = 0; s < 256; s++) w.count[s] = 0;
+    for (size_t i = 0; i < n; i++) w.count[lit[i]]++;
+    unsigned maxSym = 255;
+    while (w.count[maxSym] == 0) maxSym--;
+    uint32_t largest = 0;
+    for (unsigned s = 0; s <= maxSym; s++) if (w.count[s] > largest) largest = w.count[s];
+    if (largest == n) {  // single symbol: RLE literals block
+        size_t fl = write_rawrle_lit_header(dst, n, kSetRle);
+        dst[fl] = lit[0];
+        return fl + 1;
+    }
+    if (largest <= (n >> 7) + 4) return write_raw_literals(dst, lit, n);
+    unsigned huffLog = huf_optimal_table_log(kHufTableLogDefault, n, maxSym);
+    for (int i = 0; i < 2 * 256 + 1; i++) { w.nodes[i].count = 0; w.nodes[i].parent = 0; w.nodes[i].byte = 0; w.nodes[i].nbBits = 0; }
+    huf_sort_serial(w.nodes + 1, w.count, maxSym);
+    huffLog = huf_build_from_sorted(w.nodes, maxSym, huffLog, w.nbBits, w.val);
+    uint8_t* op = dst + lhSize;
+    size_t hSize = huf_write_ctable(op, w.nbBits, maxSym, huffLog, w.fct, w.scratch);
+    if (hSize == 0) return write_raw_literals(dst, lit, n);   // HUF error -> raw
+    if (hSize + 12 >= n) return write_raw_literals(dst, lit, n);
+    size_t cSize;
+    if (singleStream) {
+        cSize = huf_encode_1x(op + hSize, lit, n, w.nbBits, w.val);
+    } else {
+        const size_t seg = (n + 3) / 4;
+        uint8_t* jt = op + hSize;
+        uint8_t* sp = jt + 6;
+        for (int k = 0; k < 4; k++) {
+            size_t a = seg * (size_t)k, b = (k == 3) ? n : seg * (size_t)(k + 1);
+            size_t c = huf_encode_1x(sp, lit + a, b - a, w.nbBits, w.val);
+            if (k < 3) wr16(jt + 2 * k, (uint32_t)c);
+            sp += c;
+        }
+        cSize = (size_t)(sp - (op + hSize));
+    }
+    size_t total = hSize + cSize;
+    if (total >= n - 1) return write_raw_literals(dst, lit, n);        // HUF_compressCTable_internal
+    if (total >= n - minGain) return write_raw_literals(dst, lit, n);  // ZSTD_compressLiterals
+    write_huf_lit_header(dst, lhSize, n, total, singleStream);
+    return lhSize + total;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sequences section (ZSTD_compressSequences_internal, repeat mode none).  Returns bytes written,
+// or (size_t)-1 for "emit a raw block" (the <= 1.3.4 decoder workaround).
+// ---------------------------------------------------------------------------------------------
+struct SeqWork {
+    FseCTable ll, of, ml;
+    uint8_t tableSymbol[512];
+    uint32_t count[kMaxML + 1];
+    int16_t norm[kMaxML + 1];
+};
+
+PGN_HD size_t build_seq_table(uint8_t* op, FseCTable& ct, unsigned type, uint32_t* count, unsigned max,
+                              unsigned lastCode, size_t nbSeq, unsigned fseLog, unsigned defaultNormLog,
+                              unsigned defaultMax, int kind, SeqWork& w)
+{
+    if (type == kSetRle) {
+        fse_build_ctable_rle(ct, max);
+        op[0] = (uint8_t)lastCode;  // codeTable[0]; all codes are equal
+        return 1;
+    }
+    if (type == kSetBasic) {
+        for (unsigned s = 0; s <= defaultMax; s++)
+            w.norm[s] = kind == 0 ? ll_default_norm(s) : (kind == 1 ? of_default_norm(s) : ml_default_norm(s));
+        fse_build_ctable(ct, w.norm, defaultMax, defaultNormLog, w.tableSymbol);
+        return 0;
+    }
+    // compressed
+    size_t nbSeq_1 = nbSeq;
+    unsigned tableLog = fse_optimal_table_log(fseLog, nbSeq, max, 2);
+    if (count[lastCode] > 1) { count[lastCode]--; nbSeq_1--; }
+    if (!fse_normalize(w.norm, tableLog, count, nbSeq_1, max, nbSeq_1 >= 2048)) return (size_t)-2;
+    size_t nc = fse_write_ncount(op, w.norm, max, tableLog);
+    if (nc == 0) return (size_t)-2;
+    fse_build_ctable(ct, w.norm, max, tableLog, w.tableSymbol);
+    return nc;
+}
+
+// codes: ll/of/ml code per sequence (filled here)
+PGN_HD size_t compress_sequences(uint8_t* dst, const Seq* seqs, size_t nbSeq, uint8_t* llC, uint8_t* ofC,
+                                 uint8_t* mlC, SeqWork& w)
+{
+    uint8_t* op = dst;
+    if (nbSeq < 128) {
+        *op++ = (uint8_t)nbSeq;
+    } else if (nbSeq < 0x7F00) {
+        op[0] = (uint8_t)((nbSeq >> 8) + 0x80);
+        op[1] = (uint8_t)nbSeq;
+        op += 2;
+    } else {
+        op[0] = 0xFF;
+        wr16(op + 1, (uint32_t)(nbSeq - 0x7F00));
+        op += 3;
+    }
+    if (nbSeq == 0) return (size_t)(op - dst);
+    uint8_t* seqHead = op++;
+    for (size_t i = 0; i < nbSeq; i++) {
+        llC[i] = (uint8_t)ll_code(seqs[i].litLength);
+        ofC[i] = (uint8_t)highbit32(seqs[i].offset);
+        mlC[i] = (uint8_t)ml_code(seqs[i].mlBase);
+    }
+    uint8_t* lastNCount = nullptr;
+    unsigned types[3];
+    FseCTable* cts[3] = {&w.ll, &w.of, &w.ml};
+    const uint8_t* codes[3] = {llC, ofC, mlC};
+    const unsigned maxes[3] = {kMaxLL, kMaxOff, kMaxML};
+    const unsigned fseLogs[3] = {kLLFSELog, kOffFSELog, kMLFSELog};
+    const unsigned normLogs[3] = {kLLDefaultNormLog, kOFDefaultNormLog, kMLDefaultNormLog};
+    const unsigned defMax[3] = {kMaxLL, kDefaultMaxOff, kMaxML};
+    for (int k = 0; k < 3; k++) {
+        // HIST_countFast_wksp
+        for (unsigned s = 0; s <= kMaxML; s++) w.count[s] = 0;
+        for (size_t i = 0; i < nbSeq; i++) w.count[codes[k][i]]++;
+        unsigned max = maxes[k];
+        while (max > 0 && w.count[max] == 0) max--;
+        uint32_t mostFrequent = 0;
+        for (unsigned s = 0; s <= max; s++) if (w.count[s] > mostFrequent) mostFrequent = w.count[s];
+        bool defaultAllowed = (k == 1) ? (max <= kDefaultMaxOff) : true;
+        types[k] = select_encoding_type(mostFrequent, nbSeq, normLogs[k], defaultAllowed);
+        size_t sz = build_seq_table(op, *cts[k], types[k], w.count, max, codes[k][nbSeq - 1], nbSeq, fseLogs[k],
+                                    normLogs[k], defMax[k], k, w);
+        if (sz == (size_t)-2) return (size_t)-2;
+        if (types[k] == kSetCompressed) lastNCount = op;
+        op += sz;
+    }
+    *seqHead = (uint8_t)((types[0] << 6) + (types[1] << 4) + (types[2] << 2));
+    // ZSTD_encodeSequences (no long offsets: windowLog <= 17)
+    BitW bw;
+    bw_init(bw, op);
+    FseState sLL, sOF, sML;
+    const size_t last = nbSeq - 1;
+    fse_init_state2(sML, w.ml, mlC[last]);
+    fse_init_state2(sOF, w.of, ofC[last]);
+    fse_init_state2(sLL, w.ll, llC[last]);
+    bw_add(bw, seqs[last].litLength, ll_bits(llC[last]));
+    bw_add(bw, seqs[last].mlBase, ml_bits(mlC[last]));
+    bw_add(bw, seqs[last].offset, ofC[last]);
+    for (size_t n = nbSeq - 1; n-- > 0;) {
+        fse_encode(bw, sOF, w.of, ofC[n]);
+        fse_encode(bw, sML, w.ml, mlC[n]);
+        fse_encode(bw, sLL, w.ll, llC[n]);
+        bw_add(bw, seqs[n].litLength, ll_bits(llC[n]));
+        bw_add(bw, seqs[n].mlBase, ml_bits(mlC[n]));
+        bw_add(bw, seqs[n].offset, ofC[n]);
+    }
+    fse_flush(bw, sML, w.ml);
+    fse_flush(bw, sOF, w.of);
+    fse_flush(bw, sLL, w.ll);
+    size_t streamSize = bw_close(bw, op);
+    op += streamSize;
+    if (lastNCount && (op - lastNCount) < 4) return (size_t)-1;
+    return (size_t)(op - dst);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Block + frame around pre-computed sections.
+// ---------------------------------------------------------------------------------------------
+PGN_HD size_t write_empty_frame(uint8_t* dst)
+{
+    size_t h = write_frame_header(dst, 0);
+    wr24(dst + h, 1u + (kBtRaw << 1));
+    return h + 3;
+}
+PGN_HD size_t write_raw_block_frame(uint8_t* dst, const uint8_t* src, size_t n)
+{
+    size_t h = write_frame_header(dst, n);
+    wr24(dst + h, (uint32_t)(1u + (kBtRaw << 1) + (n << 3)));
+    for (size_t i = 0; i < n; i++) dst[h + 3 + i] = src[i];
+    return h + 3 + n;
+}
+
+struct CompressWork {
+    LitWork lit;
+    SeqWork seq;
+};
+
+// Full serial ZSTD_compress(dst, bound, src, n, 1) for n <= kMaxSrc.  `ht`: 2^15 entries;
+// `seqs`, `llC/ofC/mlC`: n/4 + 1 entries; `litbuf`: n bytes.  dst capacity >= compress_bound(n).
+PGN_HD size_t compress_serial(uint8_t* dst, const uint8_t* src, size_t n, uint32_t* ht, Seq* seqs, uint8_t* llC,
+                              uint8_t* ofC, uint8_t* mlC, uint8_t* litbuf, CompressWork& w)
+{
+    if (n == 0) return write_empty_frame(dst);
+    if (n < 7) return write_raw_block_frame(dst, src, n);
+    Params p = level1_params(n);
+    size_t lastLL = 0;
+    size_t nbSeq = fast_search_serial(src, n, p, ht, seqs, &lastLL);
+    // gather literals
+    const uint8_t* lit = src;
+    size_t nLit = n;
+    if (nbSeq > 0) {
+        size_t pos = 0, o = 0;
+        for (size_t i = 0; i < nbSeq; i++) {
+            for (uint32_t k = 0; k < seqs[i].litLength; k++) litbuf[o++] = src[pos + k];
+            pos += seqs[i].litLength + seqs[i].mlBase + 3;
+        }
+        for (size_t k = 0; k < lastLL; k++) litbuf[o++] = src[pos + k];
+        lit = litbuf;
+        nLit = o;
+    }
+    size_t h = frame_header_size(n);
+    uint8_t* body = dst + h + 3;
+    size_t litSize = compress_literals(body, lit, nLit, w.lit);
+    size_t seqSize = compress_sequences(body + litSize, seqs, nbSeq, llC, ofC, mlC, w.seq);
+    size_t maxCSize = n - ((n >> 6) + 2);
+    if (seqSize == (size_t)-1 || seqSize == (size_t)-2 || litSize + seqSize >= maxCSize)
+        return write_raw_block_frame(dst, src, n);
+    size_t cSize = litSize + seqSize;
+    write_frame_header(dst, n);
+    wr24(dst + h, (uint32_t)(1u + (kBtCompressed << 1) + (cSize << 3)));
+    return h + 3 + cSize;
+}
+
+}  // namespace z1
+}  // namespace pgn
