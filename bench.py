@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Benchmark: pgnano C5 encode+decode throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): synthetic reads of 100,000 int16 samples (one POD5 chunk each,
+below the 102,400 default chunk size), 100,000 reads per GPU, generated on the device by the same
+integer-only generator the checker uses.  One step = encode every chunk + decode every blob, with
+inputs already resident in HBM.  value = samples / (t_enc + t_dec) over all ranks (weak scaling:
+each rank owns its own 100k-read shard; reads are assigned round-robin, read r -> rank r % N).
+
+The dominant kernel's roofline is measured live with HIP events on the launch stream; the CPU
+baseline is the oracle (the libzstd-backed C restatement of the reference's C5 path) on one host
+thread over a bounded sample.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--samples S]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MSamples/s encode+decode (1/2/4/8 GPU) at fixed ratio; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--reads", type=int, default=100_000, help="reads per GPU")
+    p.add_argument("--samples", type=int, default=100_000, help="samples per read")
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--cpu-sample-reads", type=int, default=600)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(samples_per_read: int, nreads: int, seed: int):
+    """Oracle (C restatement of C5.hpp:282-683 over libzstd 1.4.x) on one host thread."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import _oracle as O
+
+    L = O.oracle()
+    xs = [O.synth_read(r, samples_per_read, seed=seed) for r in range(nreads)]
+    cap = L.pgno_c5_bound(samples_per_read)
+    out = np.zeros(cap, np.uint8)
+    back = np.zeros(samples_per_read, np.int16)
+    ol = C.c_size_t(0)
+    blobs = []
+    t0 = time.perf_counter()
+    for x in xs:
+        rc = L.pgno_c5_compress(x.ctypes.data, x.size, out.ctypes.data, cap, C.byref(ol), None)
+        assert rc == 0
+        blobs.append(out[: ol.value].copy())
+    t1 = time.perf_counter()
+    for b in blobs:
+        rc = L.pgno_c5_decompress(b.ctypes.data, b.size, back.ctypes.data, samples_per_read)
+        assert rc == 0
+    t2 = time.perf_counter()
+    n = samples_per_read * nreads
+    return {
+        "value": n / ((t1 - t0) + (t2 - t1)) / 1e6,
+        "unit": "MSamples/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{nreads} synthetic reads x {samples_per_read} samples (same generator), oracle C5 "
+                  f"encode {n / (t1 - t0) / 1e6:.1f} + decode {n / (t2 - t1) / 1e6:.1f} MS/s, "
+                  f"libzstd {L.pgno_zstd_version()}",
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    from rawnanoporesignalcompression_amd import PGNanoCodec
+
+    codec = PGNanoCodec(local)
+    R, S = args.reads, args.samples
+    # this rank's shard: global reads rank, rank + world, ... (round-robin)
+    samples = torch.empty(R * S, dtype=torch.int16, device="cuda")
+    counts = torch.full((R,), S, dtype=torch.int32, device="cuda")
+    offs = torch.arange(R, dtype=torch.int64, device="cuda") * S
+    codec.synth_reads(R, S, seed=args.seed, first_read=rank, read_stride=world, out=samples)
+    torch.cuda.synchronize()
+    caps = torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
+    boffs = torch.zeros(R, dtype=torch.int64, device="cuda")
+    boffs[1:] = torch.cumsum(caps, 0)[:-1]
+    blobs = torch.empty(int(caps.sum().item()), dtype=torch.uint8, device="cuda")
+    decoded = torch.empty(R * S, dtype=torch.int16, device="cuda")
+
+    def step():
+        enc = codec.compress_batch(samples, offs, counts, out=blobs, out_offsets=boffs, out_caps=caps,
+                                   stream=codec.stream)
+        codec.decompress_batch(blobs, boffs, enc.sizes, counts, out=decoded, out_offsets=offs,
+                               stream=codec.stream)
+        return enc
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    enc_ms, dec_ms = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        enc = step()
+        enc_ms.append(codec.last_encode_ms())
+        dec_ms.append(codec.last_decode_ms())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # correctness of the timed work (outside the timed region)
+    ok = bool((enc.status == 0).all().item()) and bool(torch.equal(decoded, samples))
+    comp_bytes = int(enc.sizes.sum().item())
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    red = torch.tensor([comp_bytes, R * S, 0 if ok else 1], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(red, op=dist.ReduceOp.SUM)  # the final size/ratio reduction (RCCL over xGMI)
+    elapsed = float(t.item())
+    comp_total, samples_total, errors = (int(v) for v in red.tolist())
+    if rank == 0:
+        ms_per_step = 1e3 * elapsed / args.steps
+        value = samples_total * args.steps / elapsed / 1e6
+        c_per_sample = comp_total / samples_total
+        e_ms = sum(enc_ms) / len(enc_ms)
+        d_ms = sum(dec_ms) / len(dec_ms)
+        dominant = "c5_decode_kernel" if d_ms >= e_ms else "c5_encode_kernel"
+        k_ms = max(e_ms, d_ms)
+        algo_bytes = (2.0 + comp_bytes / (R * S)) * R * S  # per launch on this GPU
+        achieved = algo_bytes / (k_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("reads") == R and tj.get("samples") == S:
+                traffic = tj.get(dominant)
+        except (OSError, ValueError):
+            pass
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "MSamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int16",
+            "data": "synthetic (device generator: piecewise-constant levels + N(0,12) noise, integer-only)",
+            "config": {
+                "workload": f"configs[1]: {R} reads x {S} int16 samples per GPU (1 chunk each), C5 encode+decode",
+                "reads_per_gpu": R,
+                "samples_per_read": S,
+                "parallelism": f"dp{world} (reads round-robin, no data-path collective)",
+            },
+            "encode_ms": round(e_ms, 3),
+            "decode_ms": round(d_ms, 3),
+            "encode_msamples_s": round(R * S / e_ms / 1e3, 1),
+            "decode_msamples_s": round(R * S / d_ms / 1e3, 1),
+            "bits_per_sample": round(8.0 * c_per_sample, 4),
+            "round_trip_ok": errors == 0,
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dominant,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+            },
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(S, args.cpu_sample_reads, args.seed) if world == 1 else None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    codec.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,111 @@
+/*
+ * pgnano_hip.h -- C ABI of the MI355X (gfx950) pgnano "C5" signal codec.
+ *
+ * Drop-in boundary for the reference's per-chunk plugin surface (tomas-gr/RawNanoporeSignalCompression):
+ *   pgnano::compress_signal   pod5/c++/pod5_format/pgnano/pgnano.h:19-23, pgnano.cpp:59-96
+ *   pgnano::decompress_signal pod5/c++/pod5_format/pgnano/pgnano.h:13-17, pgnano.cpp:98-126
+ * and of the pod5 C-API entry points built on it (pod5/c++/pod5_format/c_api.h:676-712,
+ * c_api.cpp:1177-1273).  The compressed bytes are identical to the reference's default
+ * COMPRESSOR_C5 variant (pgnano/svb16/C5.hpp:282-683) with libzstd 1.4.8/1.4.9 level 1.
+ *
+ * Plain pointers and sizes only.  Functions taking `d_` pointers expect device (HBM) memory and are
+ * asynchronous on the given HIP stream (`stream` is a hipStream_t, NULL = the context's stream);
+ * the others take host memory and are synchronous.  Every function returns a pgn_status.
+ */
+#ifndef PGNANO_HIP_H
+#define PGNANO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum pgn_status {
+    PGN_OK = 0,
+    PGN_ERR_DST_TOO_SMALL = 1,    /* "Not enough space in destination buffer"       C5.hpp:420-427 */
+    PGN_ERR_NOT_ZSTD = 2,         /* "Input data not compressed by zstd"            C5.hpp:495-502 */
+    PGN_ERR_ZSTD_DECOMPRESS = 3,  /* "Input data failed to decompress using zstd"   C5.hpp:593-600 */
+    PGN_ERR_REMAINING = 4,        /* "Remaining data at end of signal buffer"       C5.hpp:675-677 */
+    PGN_ERR_ZSTD_COMPRESS = 5,    /* "Failed to compress ..."                        C5.hpp:340-342 */
+    PGN_ERR_CORRUPT = 6,          /* input on which the reference reads out of bounds (UB there) */
+    PGN_ERR_UNSUPPORTED = 9,      /* chunk larger than PGN_MAX_CHUNK_SAMPLES */
+    PGN_ERR_INVALID_ARG = 10,
+    PGN_ERR_HIP = 11,             /* HIP runtime failure (message in pgn_last_error) */
+    PGN_ERR_NO_DEVICE = 12
+} pgn_status;
+
+/* Largest chunk the GPU path encodes (one zstd block per stream).  The reference writer's default
+ * chunk is 102,400 samples (pod5/c++/pod5_format/file_writer.h:22). */
+#define PGN_MAX_CHUNK_SAMPLES 131072u
+
+/* Per-chunk statistics, the reference's global byte counters (src/c++/copy.cpp:64-85, updated at
+ * C5.hpp:318-324,467-471): raw stream sizes then frame sizes, order keys, S, M, Llow, Lhigh. */
+#define PGN_STATS_PER_CHUNK 10
+
+typedef struct pgn_ctx pgn_ctx;
+
+/* Message of a status code (the reference's arrow::Status text where one exists). */
+const char *pgn_status_string(int status);
+/* Detail of the last PGN_ERR_HIP on this thread. */
+const char *pgn_last_error(void);
+
+/* Context bound to one HIP device (one process per GPU): scratch memory and a stream. */
+int pgn_ctx_create(int device, pgn_ctx **out);
+int pgn_ctx_destroy(pgn_ctx *ctx);
+/* The context's HIP stream (hipStream_t). */
+void *pgn_ctx_stream(pgn_ctx *ctx);
+
+/* pgnano::Compressor::compressed_signal_max_size (pgnano/compressor.h:39-45):
+ * max(2n + 26, 1024) -- the destination size pgnano::compress_signal allocates. */
+size_t pgn_compressed_signal_max_size(size_t sample_count);
+
+/* pgnano::compress_signal (pgnano.cpp:59-96) -> compress_signal_N01 (C5.hpp:282-474), host memory.
+ * dst_capacity plays the role of the destination span; *out_size gets the blob size (or, on
+ * PGN_ERR_DST_TOO_SMALL, the required size the reference prints at C5.hpp:423-424). */
+int pgn_compress_signal(pgn_ctx *ctx, const int16_t *samples, size_t sample_count, uint8_t *dst,
+                        size_t dst_capacity, size_t *out_size);
+
+/* pgnano::decompress_signal (pgnano.cpp:98-126) -> decompress_signal_N01 (C5.hpp:477-683), host
+ * memory; sample_count is the destination span size (the POD5 `samples` column). */
+int pgn_decompress_signal(pgn_ctx *ctx, const uint8_t *compressed, size_t compressed_size, int16_t *dst,
+                          size_t sample_count);
+
+/* pod5_pinanoraw_compress_signal (c_api.h:696-700, c_api.cpp:1217-1253) on a default context of
+ * device 0: *compressed_signal_size is the buffer size on input, the blob size on output. */
+int pgn_pinanoraw_compress_signal(const int16_t *signal, size_t signal_size, char *compressed_signal_out,
+                                  size_t *compressed_signal_size);
+
+/* Batched, device-resident encode of `nchunks` independent chunks (each <= PGN_MAX_CHUNK_SAMPLES):
+ * chunk i = d_samples[d_sample_offsets[i] .. + d_sample_counts[i]) -> d_out[d_out_offsets[i] ..),
+ * capacity d_out_caps[i]; d_out_sizes[i] and d_status[i] receive the result.  d_stats (optional)
+ * receives PGN_STATS_PER_CHUNK uint64 per chunk. */
+int pgn_compress_batch_device(pgn_ctx *ctx, size_t nchunks, const int16_t *d_samples,
+                              const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts, uint8_t *d_out,
+                              const uint64_t *d_out_offsets, const uint64_t *d_out_caps, uint64_t *d_out_sizes,
+                              int32_t *d_status, uint64_t *d_stats, void *stream);
+
+/* Batched, device-resident decode: blob i = d_in[d_in_offsets[i] .. + d_in_sizes[i]) ->
+ * d_samples[d_sample_offsets[i] .. + d_sample_counts[i]). */
+int pgn_decompress_batch_device(pgn_ctx *ctx, size_t nchunks, const uint8_t *d_in, const uint64_t *d_in_offsets,
+                                const uint64_t *d_in_sizes, int16_t *d_samples, const uint64_t *d_sample_offsets,
+                                const uint32_t *d_sample_counts, int32_t *d_status, void *stream);
+
+/* Device generator of the synthetic nanopore-like reads used by bench.py (integer-only, identical
+ * to the checker's pgno_synth_read): global read first_read + r * read_stride ->
+ * d_samples[d_sample_offsets[r] .. + d_sample_counts[r]). */
+int pgn_synth_reads_device(pgn_ctx *ctx, size_t nreads, uint64_t seed, uint64_t first_read, uint64_t read_stride,
+                           int16_t *d_samples,
+                           const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts,
+                           uint32_t p_switch_q16, int32_t level_mean, int32_t level_sd, int32_t noise_sd, void *stream);
+
+/* Kernel time (ms, HIP events on the launch stream) of the last batch encode / decode call on ctx. */
+float pgn_ctx_last_encode_ms(pgn_ctx *ctx);
+float pgn_ctx_last_decode_ms(pgn_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PGNANO_HIP_H */

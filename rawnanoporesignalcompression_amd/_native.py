@@ -1,0 +1,79 @@
+"""ctypes binding of the gfx950 codec library (include/pgnano_hip.h).
+
+The product path has no CPU fallback: if ``_build/libpgnano_hip.so`` is missing or cannot be
+loaded, every entry point raises :class:`NativeLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libpgnano_hip.so")
+
+PGN_OK = 0
+PGN_ERR_DST_TOO_SMALL = 1
+PGN_ERR_NOT_ZSTD = 2
+PGN_ERR_ZSTD_DECOMPRESS = 3
+PGN_ERR_REMAINING = 4
+PGN_ERR_ZSTD_COMPRESS = 5
+PGN_ERR_CORRUPT = 6
+PGN_ERR_UNSUPPORTED = 9
+PGN_ERR_INVALID_ARG = 10
+PGN_ERR_HIP = 11
+PGN_ERR_NO_DEVICE = 12
+
+PGN_MAX_CHUNK_SAMPLES = 131072
+PGN_STATS_PER_CHUNK = 10
+
+# every symbol include/pgnano_hip.h declares: (name, restype, argtypes)
+_VP, _SZ, _U64P, _U32P, _I32P = C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p
+SIGNATURES = [
+    ("pgn_status_string", C.c_char_p, [C.c_int]),
+    ("pgn_last_error", C.c_char_p, []),
+    ("pgn_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("pgn_ctx_destroy", C.c_int, [_VP]),
+    ("pgn_ctx_stream", C.c_void_p, [_VP]),
+    ("pgn_compressed_signal_max_size", C.c_size_t, [C.c_size_t]),
+    ("pgn_compress_signal", C.c_int, [_VP, _VP, _SZ, _VP, _SZ, C.POINTER(C.c_size_t)]),
+    ("pgn_decompress_signal", C.c_int, [_VP, _VP, _SZ, _VP, _SZ]),
+    ("pgn_pinanoraw_compress_signal", C.c_int, [_VP, _SZ, _VP, C.POINTER(C.c_size_t)]),
+    ("pgn_compress_batch_device", C.c_int,
+     [_VP, _SZ, _VP, _U64P, _U32P, _VP, _U64P, _U64P, _U64P, _I32P, _U64P, _VP]),
+    ("pgn_decompress_batch_device", C.c_int, [_VP, _SZ, _VP, _U64P, _U64P, _VP, _U64P, _U32P, _I32P, _VP]),
+    ("pgn_synth_reads_device", C.c_int,
+     [_VP, _SZ, C.c_uint64, C.c_uint64, C.c_uint64, _VP, _U64P, _U32P, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
+      _VP]),
+    ("pgn_ctx_last_encode_ms", C.c_float, [_VP]),
+    ("pgn_ctx_last_decode_ms", C.c_float, [_VP]),
+]
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load (once) and return the codec library; raise if it is not built."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise NativeLibraryError(
+                f"{p} is missing: build it with `make -C rawnanoporesignalcompression_amd` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        lib = C.CDLL(p)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib

@@ -1,0 +1,233 @@
+"""Host-side mirror of the reference's pgnano plugin surface, over the C ABI.
+
+Reference interface (tomas-gr/RawNanoporeSignalCompression):
+
+* ``pgnano::compress_signal(samples, pool, read_data, is_last_batch) -> Result<Buffer>``
+  (pod5/c++/pod5_format/pgnano/pgnano.h:19-23, pgnano.cpp:59-96): allocates
+  ``compressed_signal_max_size`` bytes, runs the compiled variant (C5, C5.hpp:282-474), returns the
+  resized buffer or an ``Invalid`` status.
+* ``pgnano::decompress_signal(compressed, pool, destination, state) -> Status``
+  (pgnano.h:13-17, pgnano.cpp:98-126 -> C5.hpp:477-683).
+* ``pod5_pinanoraw_compress_signal`` (c_api.cpp:1217-1253).
+
+``read_data`` / ``is_last_batch`` / ``state`` are accepted and ignored, exactly as C5 ignores them.
+Errors raise :class:`PGNanoError` carrying the reference's status message.
+
+The batched device API (:meth:`PGNanoCodec.compress_batch` / :meth:`decompress_batch`) takes
+device-resident torch tensors: one launch encodes or decodes every chunk of a batch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+
+MAX_CHUNK_SAMPLES = _native.PGN_MAX_CHUNK_SAMPLES
+
+
+class PGNanoError(RuntimeError):
+    """Mirrors the reference's ``arrow::Status::Invalid`` results."""
+
+    def __init__(self, status: int, detail: str = ""):
+        lib = _native.load()
+        msg = lib.pgn_status_string(status).decode()
+        if status == _native.PGN_ERR_HIP:
+            msg += ": " + lib.pgn_last_error().decode()
+        if detail:
+            msg += f" ({detail})"
+        super().__init__(msg)
+        self.status = status
+
+
+def _check(rc: int, detail: str = "") -> None:
+    if rc != _native.PGN_OK:
+        raise PGNanoError(rc, detail)
+
+
+def compressed_signal_max_size(sample_count: int) -> int:
+    """``pgnano::Compressor::compressed_signal_max_size`` (compressor.h:39-45)."""
+    return int(_native.load().pgn_compressed_signal_max_size(sample_count))
+
+
+def _ptr(t) -> int:
+    return t.data_ptr() if t is not None else 0
+
+
+@dataclass
+class EncodedBatch:
+    blobs: "object"          # torch.uint8 device tensor holding every blob at its offset
+    offsets: "object"        # torch.uint64 (as int64) blob offsets
+    caps: "object"           # capacities used (compressed_signal_max_size per chunk)
+    sizes: "object"          # blob sizes
+    status: "object"         # int32 status per chunk
+    stats: "object | None"   # (nchunks, 10) raw + frame sizes per stream
+
+
+class PGNanoCodec:
+    """One codec context per HIP device (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _native.load()
+        h = C.c_void_p()
+        _check(self._lib.pgn_ctx_create(int(device), C.byref(h)), f"device {device}")
+        self._h = h
+        self.device = int(device)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.pgn_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return int(self._lib.pgn_ctx_stream(self._h) or 0)
+
+    # ---- per-chunk plugin surface (host memory) -------------------------------------------
+    def compress_signal(self, samples, read_data=None, is_last_batch: bool = False) -> bytes:
+        x = np.ascontiguousarray(samples, dtype=np.int16)
+        cap = compressed_signal_max_size(x.size)
+        out = np.empty(cap, dtype=np.uint8)
+        size = C.c_size_t(0)
+        rc = self._lib.pgn_compress_signal(self._h, x.ctypes.data, x.size, out.ctypes.data, cap, C.byref(size))
+        if rc == _native.PGN_ERR_DST_TOO_SMALL:
+            raise PGNanoError(rc, f"Destination size: {cap}, Required size: {size.value}")
+        _check(rc)
+        return out[: size.value].tobytes()
+
+    def decompress_signal(self, compressed, destination=None, state=None, sample_count: int | None = None):
+        src = np.frombuffer(bytes(compressed), dtype=np.uint8)
+        if destination is None:
+            if sample_count is None:
+                raise ValueError("need a destination array or sample_count")
+            destination = np.empty(int(sample_count), dtype=np.int16)
+        if destination.dtype != np.int16 or not destination.flags.c_contiguous:
+            raise ValueError("destination must be a contiguous int16 array")
+        _check(self._lib.pgn_decompress_signal(self._h, src.ctypes.data if src.size else 0, src.size,
+                                               destination.ctypes.data, destination.size))
+        return destination
+
+    # ---- batched device API -----------------------------------------------------------------
+    def compress_batch(self, samples, sample_offsets, sample_counts, with_stats: bool = False,
+                       out=None, out_offsets=None, out_caps=None, stream: int | None = None) -> EncodedBatch:
+        """Encode every chunk of a device-resident batch in one launch.
+
+        samples: int16 cuda tensor; sample_offsets: int64 tensor (elements); sample_counts: int32.
+        Blobs land at ``out_offsets`` (default: packed with compressed_signal_max_size capacities).
+        """
+        import torch
+
+        dev = samples.device
+        n = int(sample_counts.numel())
+        counts = sample_counts.to(device=dev, dtype=torch.int32).contiguous()
+        offs = sample_offsets.to(device=dev, dtype=torch.int64).contiguous()
+        if out_caps is None:
+            caps = torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
+        else:
+            caps = out_caps.to(device=dev, dtype=torch.int64).contiguous()
+        if out_offsets is None:
+            oo = torch.zeros(n, dtype=torch.int64, device=dev)
+            if n > 1:
+                oo[1:] = torch.cumsum(caps, 0)[:-1]
+        else:
+            oo = out_offsets.to(device=dev, dtype=torch.int64).contiguous()
+        if out is None:
+            total = int((oo[-1] + caps[-1]).item()) if n else 0
+            out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+        sizes = torch.zeros(n, dtype=torch.int64, device=dev)
+        status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        stats = torch.zeros((n, _native.PGN_STATS_PER_CHUNK), dtype=torch.int64, device=dev) if with_stats else None
+        _check(self._lib.pgn_compress_batch_device(
+            self._h, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
+            _ptr(status), _ptr(stats), stream or 0))
+        return EncodedBatch(out, oo, caps, sizes, status, stats)
+
+    def decompress_batch(self, blobs, blob_offsets, blob_sizes, sample_counts, out=None, out_offsets=None,
+                         stream: int | None = None):
+        """Decode a device-resident batch; returns (samples int16 tensor, offsets, status)."""
+        import torch
+
+        dev = blobs.device
+        n = int(sample_counts.numel())
+        counts = sample_counts.to(device=dev, dtype=torch.int32).contiguous()
+        if out_offsets is None:
+            so = torch.zeros(n, dtype=torch.int64, device=dev)
+            if n > 1:
+                so[1:] = torch.cumsum(counts.to(torch.int64), 0)[:-1]
+        else:
+            so = out_offsets.to(device=dev, dtype=torch.int64).contiguous()
+        if out is None:
+            total = int(counts.to(torch.int64).sum().item())
+            out = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
+        status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        _check(self._lib.pgn_decompress_batch_device(
+            self._h, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
+            _ptr(blob_sizes.to(torch.int64).contiguous()), _ptr(out), _ptr(so), _ptr(counts), _ptr(status),
+            stream or 0))
+        return out, so, status
+
+    def synth_reads(self, nreads: int, samples_per_read, seed: int = 42, first_read: int = 0, read_stride: int = 1,
+                    p_switch_q16: int = 6554, level_mean: int = 500, level_sd: int = 60, noise_sd: int = 12,
+                    out=None):
+        """Generate synthetic reads on the device (bench input); returns (samples, offsets, counts)."""
+        import torch
+
+        dev = torch.device("cuda", self.device)
+        if isinstance(samples_per_read, int):
+            counts = torch.full((nreads,), samples_per_read, dtype=torch.int32, device=dev)
+        else:
+            counts = torch.as_tensor(samples_per_read, dtype=torch.int32, device=dev)
+        offs = torch.zeros(nreads, dtype=torch.int64, device=dev)
+        if nreads > 1:
+            offs[1:] = torch.cumsum(counts.to(torch.int64), 0)[:-1]
+        total = int(counts.to(torch.int64).sum().item())
+        if out is None:
+            out = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
+        _check(self._lib.pgn_synth_reads_device(self._h, nreads, seed, first_read, read_stride, _ptr(out), _ptr(offs),
+                                                _ptr(counts), p_switch_q16, level_mean, level_sd, noise_sd, 0))
+        return out, offs, counts
+
+    def last_encode_ms(self) -> float:
+        return float(self._lib.pgn_ctx_last_encode_ms(self._h))
+
+    def last_decode_ms(self) -> float:
+        return float(self._lib.pgn_ctx_last_decode_ms(self._h))
+
+
+_default: PGNanoCodec | None = None
+
+
+def default_codec() -> PGNanoCodec:
+    global _default
+    if _default is None:
+        _default = PGNanoCodec(0)
+    return _default
+
+
+def compress_signal(samples, pool=None, read_data=None, is_last_batch: bool = False) -> bytes:
+    """Module-level ``pgnano::compress_signal`` on the default device."""
+    return default_codec().compress_signal(samples, read_data, is_last_batch)
+
+
+def decompress_signal(compressed, pool=None, destination=None, state=None, sample_count: int | None = None):
+    """Module-level ``pgnano::decompress_signal`` on the default device."""
+    return default_codec().decompress_signal(compressed, destination, state, sample_count)
+
+
+def pinanoraw_compress_signal(signal, buffer_size: int | None = None) -> bytes:
+    """``pod5_pinanoraw_compress_signal`` (c_api.cpp:1217-1253)."""
+    lib = _native.load()
+    x = np.ascontiguousarray(signal, dtype=np.int16)
+    cap = buffer_size if buffer_size is not None else compressed_signal_max_size(x.size)
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    size = C.c_size_t(cap)
+    _check(lib.pgn_pinanoraw_compress_signal(x.ctypes.data, x.size, out.ctypes.data, C.byref(size)))
+    return out[: size.value].tobytes()

@@ -1,0 +1,487 @@
+// pgn_zenc.h -- one wave compresses one byte stream into a zstd level-1 frame that is byte-identical
+// to libzstd 1.4.8/1.4.9 `ZSTD_compress(dst, cap, src, n, 1)` (the call at C5.hpp:337-413).
+//
+// Data-parallel stages run on all 64 lanes:
+//   * the level-1 `fast` match search, speculated 64 visit positions at a time;
+//   * literal histograms (LDS atomics, one histogram per Huffman segment);
+//   * symbol ranking for the Huffman sort; per-segment bit counts;
+//   * Huffman bit packing (prefix sum of code lengths, LDS window, byte flush).
+// Serial stages (tree build, weight FSE, sequence FSE) run on lane 0 with the shared zstd1_* code.
+#pragma once
+#include "pgn_wave.h"
+#include "zstd1_model.h"
+
+namespace pgn {
+
+constexpr int kWinWords = 200;  // 512 symbols * 12 bits / 32 + carry
+
+struct EncLds {
+    uint32_t hist4[4][256];
+    uint32_t count[256];
+    uint32_t cw[256];  // Huffman code | nbBits << 16
+    z1::HufNode nodes[2 * 256 + 4];
+    uint8_t nbBits[256];
+    uint16_t val[256];
+    uint8_t weights[256];
+    uint8_t hdr[320];  // Huffman table description staged before it is known to be used
+    z1::FseCTable fct;
+    uint8_t fscratch[64];
+    uint32_t win[kWinWords];
+    uint8_t nib[272];
+    uint32_t u[8];
+};
+
+struct EncScratch {
+    uint32_t* ht;        // 2^15 tagged hash-table entries
+    z1::Seq* seqs;       // <= stream/4 + 2 sequences
+    uint8_t* codes;      // 3 * (stream/4 + 2)
+    uint8_t* lit;        // gathered literals (stream bytes)
+    uint8_t* seqSection; // sequences section staging (compress_bound(stream))
+    z1::SeqWork* seqWork;
+    uint32_t maxSeq;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Match search (ZSTD_compressBlock_fast, 1.4.x) speculated over 64 consecutive visits.
+// Table entries are (tag << 17) | index; any other tag reads as an empty slot.
+// ---------------------------------------------------------------------------------------------
+__device__ inline uint32_t wave_match_count(const uint8_t* src, uint32_t a, uint32_t b, uint32_t end)
+{
+    const int lane = lane_id();
+    uint32_t n = 0;
+    while (a + n < end) {
+        uint32_t len = end - (a + n);
+        uint32_t mism = 0xFFFFFFFFu;  // first mismatching offset within this lane's 4 bytes
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            uint32_t o = 4u * (uint32_t)lane + (uint32_t)j;
+            if (o < len && mism == 0xFFFFFFFFu && src[a + n + o] != src[b + n + o]) mism = o;
+        }
+        bool over = (4u * (uint32_t)lane + 4u > len);
+        uint64_t mm = ballot(mism != 0xFFFFFFFFu);
+        if (mm) {
+            int f = __builtin_ctzll(mm);
+            return n + readlane_u32(mism, f);
+        }
+        if (ballot(over)) return len + n;  // matched to the end
+        n += 256;
+    }
+    return n;
+}
+
+__device__ inline uint32_t tagged(uint32_t tag, uint32_t idx) { return (tag << 17) | idx; }
+
+__device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uint32_t n, const z1::Params& p,
+                                            uint32_t* __restrict__ ht, uint32_t tag, z1::Seq* __restrict__ seqs,
+                                            uint32_t* lastLL)
+{
+    const int lane = lane_id();
+    const unsigned hlog = p.hashLog, mls = p.mls;
+    const long iend = (long)n, ilimit = (long)n - 8;
+    long ip0 = 1, anchor = 0;
+    uint32_t off1 = 1, off2 = 0;
+    uint32_t nbSeq = 0;
+    while (ip0 + 1 < ilimit) {
+        // positions of the next 64 visits (the no-match recurrence)
+        long pk = ip0, q = ip0;
+        for (int k = 0; k < 64; k++) {
+            if (k == lane) pk = q;
+            q += ((q - anchor) >> 7) + 2;
+        }
+        const long pNext = q;
+        const bool valid = (pk + 1 < ilimit);
+        uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu, t0 = 0, t1 = 0;
+        if (valid) {
+            h0 = z1::hash_at(src + pk, hlog, mls);
+            h1 = z1::hash_at(src + pk + 1, hlog, mls);
+            t0 = ht[h0];
+            t1 = ht[h1];
+        }
+        // most recent in-step writer before me, first in-step writer after me
+        uint32_t m0 = 0, m1 = 0;
+        bool has0 = false, has1 = false;
+        int later0 = 64, later1 = 64;
+        for (int j = 0; j < 64; j++) {
+            uint32_t hj0 = readlane_u32(h0, j), hj1 = readlane_u32(h1, j);
+            uint32_t pj = readlane_u32((uint32_t)pk, j);
+            if (j < lane) {
+                if (hj1 == h0) { m0 = pj + 2; has0 = true; } else if (hj0 == h0) { m0 = pj + 1; has0 = true; }
+                if (hj1 == h1) { m1 = pj + 2; has1 = true; } else if (hj0 == h1) { m1 = pj + 1; has1 = true; }
+            } else if (j > lane) {
+                if (later0 == 64 && (hj0 == h0 || hj1 == h0)) later0 = j;
+                if (later1 == 64 && (hj0 == h1 || hj1 == h1)) later1 = j;
+            }
+        }
+        if (!has0) m0 = ((t0 >> 17) == tag) ? (t0 & 0x1FFFFu) : 0u;
+        if (!has1) m1 = ((t1 >> 17) == tag) ? (t1 & 0x1FFFFu) : 0u;
+        bool rep = false, c0 = false, c1 = false;
+        if (valid) {
+            const long ip2 = pk + 2;
+            rep = (off1 > 0) && (ld32u(src + ip2 - off1) == ld32u(src + ip2));
+            c0 = (m0 > 1) && (ld32u(src + m0 - 1) == ld32u(src + pk));
+            c1 = (m1 > 1) && (ld32u(src + m1 - 1) == ld32u(src + pk + 1));
+        }
+        const uint64_t hits = ballot(rep || c0 || c1);
+        const uint64_t vmask = ballot(valid);
+        const int f = hits ? __builtin_ctzll(hits) : 64;
+        const int lastCommit = hits ? f : (63 - __builtin_clzll(vmask));
+        if (valid && lane <= lastCommit) {
+            const bool w1 = later1 > lastCommit;
+            const bool w0 = (later0 > lastCommit) && (h0 != h1);
+            if (w0) ht[h0] = tagged(tag, (uint32_t)pk + 1);
+            if (w1) ht[h1] = tagged(tag, (uint32_t)pk + 2);
+        }
+        if (!hits) {
+            wave_sync();
+            if (vmask == ~0ull) { ip0 = pNext; continue; }
+            break;
+        }
+        // the match found at visit f, processed exactly as the serial loop does
+        const long ipf = (long)readlane_u32((uint32_t)pk, f);
+        const bool repf = (ballot(rep) >> f) & 1, c0f = (ballot(c0) >> f) & 1;
+        const uint32_t m0f = readlane_u32(m0, f), m1f = readlane_u32(m1, f);
+        const uint32_t cur0 = (uint32_t)ipf + 1;
+        long ipm, match0;
+        uint32_t mLength, offcode;
+        if (repf) {
+            const long ip2 = ipf + 2;
+            mLength = (src[ip2 - 1] == src[ip2 - (long)off1 - 1]) ? 1u : 0u;
+            ipm = ip2 - (long)mLength;
+            match0 = ipm - (long)off1;
+            mLength += 4;
+            offcode = 0;
+        } else {
+            if (c0f) { ipm = ipf; match0 = (long)m0f - 1; }
+            else { ipm = ipf + 1; match0 = (long)m1f - 1; }
+            off2 = off1;
+            off1 = (uint32_t)(ipm - match0);
+            offcode = off1 + 2;
+            mLength = 4;
+            while ((ipm > anchor) && (match0 > 0) && (src[ipm - 1] == src[match0 - 1])) { ipm--; match0--; mLength++; }
+        }
+        mLength += wave_match_count(src, (uint32_t)ipm + mLength, (uint32_t)match0 + mLength, (uint32_t)iend);
+        if (lane == 0) {
+            seqs[nbSeq].litLength = (uint32_t)(ipm - anchor);
+            seqs[nbSeq].offset = offcode + 1;
+            seqs[nbSeq].mlBase = mLength - 3;
+        }
+        nbSeq++;
+        ip0 = ipm + (long)mLength;
+        anchor = ip0;
+        if (ip0 <= ilimit) {
+            if (lane == 0) {
+                ht[z1::hash_at(src + cur0 + 1, hlog, mls)] = tagged(tag, cur0 + 2);
+                ht[z1::hash_at(src + ip0 - 2, hlog, mls)] = tagged(tag, (uint32_t)(ip0 - 2) + 1);
+            }
+            if (off2 > 0) {
+                while ((ip0 <= ilimit) && (ld32u(src + ip0) == ld32u(src + ip0 - off2))) {
+                    uint32_t rLength = wave_match_count(src, (uint32_t)ip0 + 4, (uint32_t)ip0 + 4 - off2, (uint32_t)iend) + 4;
+                    uint32_t t = off2; off2 = off1; off1 = t;
+                    if (lane == 0) {
+                        ht[z1::hash_at(src + ip0, hlog, mls)] = tagged(tag, (uint32_t)ip0 + 1);
+                        seqs[nbSeq].litLength = 0;
+                        seqs[nbSeq].offset = 1;
+                        seqs[nbSeq].mlBase = rLength - 3;
+                    }
+                    nbSeq++;
+                    ip0 += (long)rLength;
+                    anchor = ip0;
+                }
+            }
+        }
+        wave_sync();
+    }
+    *lastLL = (uint32_t)(iend - anchor);
+    return nbSeq;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Huffman bit packing of one segment: symbols are written last-to-first (HUF_compress1X order), so
+// the stream position of a symbol is the sum of the code lengths of the symbols after it.
+// ---------------------------------------------------------------------------------------------
+__device__ inline void huf_encode_segment_wave(uint8_t* __restrict__ out, const uint8_t* __restrict__ src, uint32_t len,
+                                               uint32_t totalBits, const uint32_t* cw, uint32_t* win)
+{
+    const int lane = lane_id();
+    for (int w = lane; w < kWinWords; w += 64) win[w] = 0;
+    wave_sync();
+    uint32_t winLo = 0;   // bit offset of win[0] (multiple of 32)
+    uint32_t bitBase = 0; // bits emitted before this step
+    for (uint32_t r0 = 0; r0 < len; r0 += 512) {
+        uint32_t code[8], nb[8];
+        uint32_t myBits = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            uint32_t r = r0 + (uint32_t)lane * 8 + (uint32_t)j;
+            nb[j] = 0;
+            code[j] = 0;
+            if (r < len) {
+                uint32_t c = cw[src[len - 1 - r]];
+                code[j] = c & 0xFFFF;
+                nb[j] = c >> 16;
+            }
+            myBits += nb[j];
+        }
+        const uint32_t incl = wave_incl_sum(myBits);
+        const uint32_t stepBits = readlane_u32(incl, 63);
+        uint32_t pos = bitBase + (incl - myBits) - winLo;  // window-relative bit position
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            uint64_t acc = 0;
+            uint32_t n = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                acc |= (uint64_t)code[4 * h + j] << n;
+                n += nb[4 * h + j];
+            }
+            if (n) {
+                uint32_t w = pos >> 5, sh = pos & 31;
+                uint64_t lo = acc << sh;
+                atomicOr(&win[w], (uint32_t)lo);
+                if (sh + n > 32) atomicOr(&win[w + 1], (uint32_t)(lo >> 32));
+                if (sh + n > 64) atomicOr(&win[w + 2], (uint32_t)(acc >> (64 - sh)));
+            }
+            pos += n;
+        }
+        wave_sync();
+        const uint32_t endRel = bitBase + stepBits - winLo;
+        const uint32_t complete = endRel >> 5;
+        uint8_t* o = out + (winLo >> 3);
+        for (uint32_t w = (uint32_t)lane; w < complete; w += 64) {
+            uint32_t v = win[w];
+            __builtin_memcpy(o + 4 * w, &v, 4);
+        }
+        const uint32_t carry = win[complete];
+        wave_sync();
+        for (uint32_t w = (uint32_t)lane; w <= complete + 3 && w < (uint32_t)kWinWords; w += 64) win[w] = 0;
+        wave_sync();
+        if (lane == 0) win[0] = carry;
+        winLo += complete * 32;
+        bitBase += stepBits;
+        wave_sync();
+    }
+    // end mark, then the last partial bytes
+    if (lane == 0) {
+        uint32_t rel = totalBits - winLo;
+        win[rel >> 5] |= 1u << (rel & 31);
+        uint32_t nbytes = ((totalBits + 8) >> 3) - (winLo >> 3);
+        uint8_t* o = out + (winLo >> 3);
+        for (uint32_t b = 0; b < nbytes; b++) o[b] = (uint8_t)(win[b >> 2] >> (8 * (b & 3)));
+    }
+    wave_sync();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Literals section (ZSTD_compressLiterals).  Writes at dst, returns its size.
+// ---------------------------------------------------------------------------------------------
+__device__ inline size_t write_raw_literals_wave(uint8_t* dst, const uint8_t* lit, uint32_t n)
+{
+    size_t fl = z1::raw_lit_header_size(n);
+    if (lane_id() == 0) z1::write_rawrle_lit_header(dst, n, z1::kSetBasic);
+    wave_copy(dst + fl, lit, n);
+    return fl + n;
+}
+
+__device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
+                                                EncLds& L)
+{
+    const int lane = lane_id();
+    if (n <= 63) return write_raw_literals_wave(dst, lit, n);
+    const uint32_t minGain = (n >> 6) + 2;
+    const uint32_t lhSize = (uint32_t)z1::huf_lit_header_size(n);
+    const bool single = n < 256;
+    const uint32_t segSize = single ? n : (n + 3) / 4;
+    const int nseg = single ? 1 : 4;
+    for (int i = lane; i < 4 * 256; i += 64) (&L.hist4[0][0])[i] = 0;
+    wave_sync();
+    // per-segment histograms
+    for (uint32_t i = (uint32_t)lane * 16; i < n; i += 1024) {
+        uint8_t b[16];
+        if (i + 16 <= n) {
+            uint4 v;
+            __builtin_memcpy(&v, lit + i, 16);
+            __builtin_memcpy(b, &v, 16);
+        } else {
+            for (int k = 0; k < 16; k++) b[k] = (i + k < n) ? lit[i + k] : 0;
+        }
+        uint32_t sa = i / segSize;
+        uint32_t boundary = (sa + 1) * segSize;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (i + k < n) {
+                uint32_t sg = (i + k < boundary) ? sa : sa + 1;
+                atomicAdd(&L.hist4[sg][b[k]], 1u);
+            }
+        }
+    }
+    wave_sync();
+    uint32_t c[4];
+    uint32_t myMaxSym = 0, myLargest = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        int s = lane + 64 * q;
+        c[q] = L.hist4[0][s] + L.hist4[1][s] + L.hist4[2][s] + L.hist4[3][s];
+        L.count[s] = c[q];
+        if (c[q]) myMaxSym = (uint32_t)s;
+        myLargest = c[q] > myLargest ? c[q] : myLargest;
+    }
+    const uint32_t maxSym = wave_max(myMaxSym);
+    const uint32_t largest = wave_max(myLargest);
+    wave_sync();
+    if (largest == n) {  // one symbol: RLE literals
+        size_t fl = z1::raw_lit_header_size(n);
+        if (lane == 0) {
+            z1::write_rawrle_lit_header(dst, n, z1::kSetRle);
+            dst[fl] = lit[0];
+        }
+        return fl + 1;
+    }
+    if (largest <= (n >> 7) + 4) return write_raw_literals_wave(dst, lit, n);
+    unsigned huffLog = z1::huf_optimal_table_log(z1::kHufTableLogDefault, n, maxSym);
+    // HUF_sort: rank = #greater + #equal-with-smaller-symbol (stable, decreasing count)
+    for (int i = lane; i < 2 * 256 + 4; i += 64) {
+        L.nodes[i].count = 0; L.nodes[i].parent = 0; L.nodes[i].byte = 0; L.nodes[i].nbBits = 0;
+    }
+    wave_sync();
+    {
+        uint32_t rank[4] = {0, 0, 0, 0};
+        for (uint32_t t = 0; t <= maxSym; t++) {
+            uint32_t ct = L.count[t];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t s = (uint32_t)lane + 64u * (uint32_t)q;
+                rank[q] += (ct > c[q]) || (ct == c[q] && t < s);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t s = (uint32_t)lane + 64u * (uint32_t)q;
+            if (s <= maxSym) { L.nodes[1 + rank[q]].count = c[q]; L.nodes[1 + rank[q]].byte = (uint8_t)s; }
+        }
+    }
+    wave_sync();
+    if (lane == 0) {
+        unsigned hl = z1::huf_build_from_sorted(L.nodes, maxSym, huffLog, L.nbBits, L.val);
+        size_t hSize = z1::huf_write_ctable(L.hdr, L.nbBits, maxSym, hl, L.fct, L.fscratch);
+        L.u[0] = hl;
+        L.u[1] = (uint32_t)hSize;
+    }
+    wave_sync();
+    const uint32_t hSize = L.u[1];
+    if (hSize == 0 || hSize + 12 >= n) return write_raw_literals_wave(dst, lit, n);
+    // exact stream sizes from the segment histograms
+    uint32_t bytes[4] = {0, 0, 0, 0}, bits[4] = {0, 0, 0, 0};
+    {
+        uint32_t b4[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int s = lane + 64 * q;
+            uint32_t nbq = ((uint32_t)s <= maxSym) ? L.nbBits[s] : 0;
+            L.cw[s] = ((uint32_t)s <= maxSym) ? ((uint32_t)L.val[s] | (nbq << 16)) : 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) b4[k] += L.hist4[k][s] * nbq;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            bits[k] = wave_sum(b4[k]);
+            bytes[k] = (bits[k] + 8) >> 3;
+        }
+    }
+    uint32_t cStreams = single ? bytes[0] : 6 + bytes[0] + bytes[1] + bytes[2] + bytes[3];
+    uint32_t total = hSize + cStreams;
+    if (total >= n - 1 || total >= n - minGain) return write_raw_literals_wave(dst, lit, n);
+    if (lane == 0) {
+        z1::write_huf_lit_header(dst, lhSize, n, total, single);
+        if (!single) {
+            z1::wr16(dst + lhSize + hSize, bytes[0]);
+            z1::wr16(dst + lhSize + hSize + 2, bytes[1]);
+            z1::wr16(dst + lhSize + hSize + 4, bytes[2]);
+        }
+    }
+    for (uint32_t i = (uint32_t)lane; i < hSize; i += 64) dst[lhSize + i] = L.hdr[i];
+    wave_sync();
+    uint8_t* op = dst + lhSize + hSize + (single ? 0 : 6);
+    for (int k = 0; k < nseg; k++) {
+        uint32_t a = segSize * (uint32_t)k;
+        uint32_t e = (k == nseg - 1) ? n : a + segSize;
+        huf_encode_segment_wave(op, lit + a, e - a, bits[k], L.cw, L.win);
+        op += bytes[k];
+    }
+    return lhSize + total;
+}
+
+// ---------------------------------------------------------------------------------------------
+// One stream -> one frame.  dst must have compress_bound(n) bytes.  Returns the frame size.
+// ---------------------------------------------------------------------------------------------
+__device__ inline size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
+                                             EncLds& L, const EncScratch& S, uint32_t tag)
+{
+    const int lane = lane_id();
+    if (n == 0) {
+        if (lane == 0) z1::write_empty_frame(dst);
+        return 9;
+    }
+    const size_t h = z1::frame_header_size(n);
+    if (n < 7) {
+        if (lane == 0) z1::write_raw_block_frame(dst, src, n);
+        return h + 3 + n;
+    }
+    const z1::Params p = z1::level1_params(n);
+    uint32_t lastLL = 0;
+    const uint32_t nbSeq = fast_search_wave(src, n, p, S.ht, tag, S.seqs, &lastLL);
+    const uint8_t* lit = src;
+    uint32_t nLit = n;
+    if (nbSeq > 0) {
+        // gather the literal runs
+        uint32_t pos = 0, o = 0;
+        for (uint32_t i = 0; i < nbSeq; i++) {
+            const z1::Seq sq = S.seqs[i];
+            wave_copy(S.lit + o, src + pos, sq.litLength);
+            o += sq.litLength;
+            pos += sq.litLength + sq.mlBase + 3;
+        }
+        wave_copy(S.lit + o, src + pos, lastLL);
+        o += lastLL;
+        wave_sync();
+        lit = S.lit;
+        nLit = o;
+    }
+    uint8_t* body = dst + h + 3;
+    const size_t litSize = compress_literals_wave(body, lit, nLit, L);
+    wave_sync();
+    size_t seqSize;
+    if (nbSeq == 0) {
+        if (lane == 0) body[litSize] = 0;
+        seqSize = 1;
+    } else {
+        if (lane == 0) {
+            size_t r = z1::compress_sequences(S.seqSection, S.seqs, nbSeq, S.codes, S.codes + S.maxSeq,
+                                              S.codes + 2 * S.maxSeq, *S.seqWork);
+            L.u[2] = (uint32_t)r;
+            L.u[3] = (r == (size_t)-1 || r == (size_t)-2) ? 1u : 0u;
+        }
+        wave_sync();
+        seqSize = L.u[3] ? (size_t)-1 : (size_t)L.u[2];
+    }
+    const size_t maxCSize = n - ((n >> 6) + 2);
+    if (seqSize == (size_t)-1 || litSize + seqSize >= maxCSize) {
+        wave_sync();
+        if (lane == 0) {
+            z1::write_frame_header(dst, n);
+            z1::wr24(dst + h, (uint32_t)(1u + (z1::kBtRaw << 1) + (n << 3)));
+        }
+        wave_copy(dst + h + 3, src, n);
+        wave_sync();
+        return h + 3 + n;
+    }
+    if (nbSeq > 0) wave_copy(body + litSize, S.seqSection, seqSize);
+    const size_t cSize = litSize + seqSize;
+    if (lane == 0) {
+        z1::write_frame_header(dst, n);
+        z1::wr24(dst + h, (uint32_t)(1u + (z1::kBtCompressed << 1) + (cSize << 3)));
+    }
+    wave_sync();
+    return h + 3 + cSize;
+}
+
+}  // namespace pgn
