@@ -134,6 +134,20 @@ size_t pgno_c5_bound(uint32_t n)
     return s > 1024u ? s : 1024u;
 }
 
+/* Reusable per-thread scratch: the reference allocates from an arrow::MemoryPool (jemalloc), which
+ * recycles these buffers between chunks; fresh malloc/mmap per call would time page faults. */
+static __thread uint8_t *tl_buf[2];
+static __thread size_t tl_cap[2];
+static uint8_t *scratch(int i, size_t n)
+{
+    if (tl_cap[i] < n) {
+        free(tl_buf[i]);
+        tl_buf[i] = (uint8_t *)malloc(n);
+        tl_cap[i] = tl_buf[i] ? n : 0;
+    }
+    return tl_buf[i];
+}
+
 static inline void put_u64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); } /* host-endian size_t */
 static inline uint64_t get_u64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v; }
 
@@ -233,7 +247,7 @@ int pgno_c5_compress(const int16_t *x, uint32_t n, uint8_t *dst, size_t cap, siz
 {
     if (!zok()) return PGNO_ERR_NO_ZSTD;
     size_t nk = ((size_t)n + 3u) / 4u;
-    uint8_t *buf = (uint8_t *)malloc(nk + 4 * (size_t)n + 16);
+    uint8_t *buf = scratch(0, nk + 4 * (size_t)n + 16);
     if (!buf) return PGNO_ERR_ALLOC;
     uint8_t *st[5];
     st[0] = buf;
@@ -245,13 +259,14 @@ int pgno_c5_compress(const int16_t *x, uint32_t n, uint8_t *dst, size_t cap, siz
     pgno_c5_split(x, n, st[0], st[1], st[2], st[3], st[4], sz);
 
     uint8_t *fr[5];
-    size_t fsz[5];
+    size_t fsz[5], fb[5], ftot = 0;
     int rc = PGNO_OK;
-    for (int s = 0; s < 5; s++) fr[s] = NULL;
+    for (int s = 0; s < 5; s++) { fb[s] = Z.bound(sz[s]); ftot += fb[s]; }
+    uint8_t *fbuf = scratch(1, ftot + 16);
+    if (!fbuf) return PGNO_ERR_ALLOC;
+    for (int s = 0, o = 0; s < 5; s++) { fr[s] = fbuf + o; o += (int)fb[s]; }
     for (int s = 0; s < 5 && rc == PGNO_OK; s++) {
-        size_t b = Z.bound(sz[s]);
-        fr[s] = (uint8_t *)malloc(b ? b : 1);
-        if (!fr[s]) { rc = PGNO_ERR_ALLOC; break; }
+        size_t b = fb[s];
         size_t r = Z.compress(fr[s], b, st[s], sz[s], 1);
         if (Z.iserror(r)) { rc = PGNO_ERR_ZSTD_COMPRESS; break; }
         fsz[s] = r;
@@ -274,8 +289,6 @@ int pgno_c5_compress(const int16_t *x, uint32_t n, uint8_t *dst, size_t cap, siz
             *out_len = total;
         }
     }
-    for (int s = 0; s < 5; s++) free(fr[s]);
-    free(buf);
     return rc;
 }
 
@@ -304,18 +317,18 @@ int pgno_c5_decompress(const uint8_t *src, size_t len, int16_t *out, uint32_t n)
     }
     uint64_t total = 0;
     for (int s = 0; s < 5; s++) total += cs[s];
-    uint8_t *inter = (uint8_t *)malloc(total ? total : 1);
+    if (total > ((uint64_t)1 << 40)) return PGNO_ERR_ALLOC;
+    uint8_t *inter = scratch(0, total ? total : 1);
     if (!inter) return PGNO_ERR_ALLOC;
     uint64_t off = 0, dres[5];
     for (int s = 0; s < 5; s++) {
         size_t r = Z.decompress(inter + off, (size_t)cs[s], fp[s], (size_t)fl[s]);
-        if (Z.iserror(r)) { free(inter); return PGNO_ERR_ZSTD_DECOMPRESS; }
+        if (Z.iserror(r)) return PGNO_ERR_ZSTD_DECOMPRESS;
         dres[s] = r;
         off += cs[s]; /* write_ptr advances by the frame content size (C5.hpp:602,618,635,652) */
     }
     uint64_t consumed = 0;
     int rc = c5_merge(inter, total, dres[1], dres[2], dres[3], out, n, &consumed);
-    free(inter);
     if (rc != PGNO_OK) return rc;
     if (consumed != total) return PGNO_ERR_REMAINING; /* padding = 0 (pgnano/svb16/decode.hpp:16-21) */
     return PGNO_OK;

@@ -65,6 +65,13 @@ def load(path: str | None = None) -> C.CDLL:
         if _lib is not None and path is None:
             return _lib
         p = path or LIB_PATH
+        # One HIP runtime per process: PyTorch ships its own libamdhip64 (soname libamdhip64.so.7,
+        # but its libraries NEED the unversioned name), so load torch first and let this library
+        # bind to the runtime torch already mapped; loading ours first would map a second runtime.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(p):
             raise NativeLibraryError(
                 f"{p} is missing: build it with `make -C rawnanoporesignalcompression_amd` "

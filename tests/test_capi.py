@@ -1,0 +1,59 @@
+"""The C ABI library loads and exports every symbol include/pgnano_hip.h declares (no GPU needed)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "pgnano_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pgn_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported_and_bound():
+    from rawnanoporesignalcompression_amd import _native
+
+    lib = _native.load()
+    names = declared_symbols()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    bound = {s[0] for s in _native.SIGNATURES}
+    assert set(names) == bound
+
+
+def test_host_only_entry_points():
+    from rawnanoporesignalcompression_amd import _native, compressed_signal_max_size
+
+    lib = _native.load()
+    # pgnano::Compressor::compressed_signal_max_size (compressor.h:39-45)
+    assert compressed_signal_max_size(0) == 1024
+    assert compressed_signal_max_size(499) == 1024
+    assert compressed_signal_max_size(500) == 1026
+    assert compressed_signal_max_size(100000) == 200026
+    assert lib.pgn_status_string(1) == b"Not enough space in destination buffer"
+    assert lib.pgn_status_string(2) == b"Input data not compressed by zstd"
+    assert lib.pgn_status_string(3) == b"Input data failed to decompress using zstd"
+    assert lib.pgn_status_string(4) == b"Remaining data at end of signal buffer"
+
+
+def test_no_device_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from rawnanoporesignalcompression_amd import PGNanoCodec, PGNanoError
+
+    with pytest.raises(PGNanoError):
+        PGNanoCodec(0)
+
+
+def test_missing_library_raises(tmp_path):
+    from rawnanoporesignalcompression_amd import NativeLibraryError, _native
+
+    with pytest.raises(NativeLibraryError):
+        _native.load(str(tmp_path / "nope.so"))

@@ -1,0 +1,98 @@
+"""The shared zstd level-1 encoder/decoder code (rawnanoporesignalcompression_amd/csrc, the code the
+GPU kernels run), built for the host, against the real libzstd -- byte for byte."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.skipif(not os.path.exists(O.MODEL_SO), reason="libpgn_model.so not built")
+
+
+def model_compress(b: np.ndarray) -> bytes:
+    M = O.model()
+    cap = O.oracle().pgno_zstd_bound(b.size)
+    out = np.zeros(cap + 16, np.uint8)
+    r = M.z1m_compress(b.ctypes.data if b.size else 0, b.size, out.ctypes.data, cap)
+    return out[:r].tobytes()
+
+
+def model_decompress(fr: bytes, n: int):
+    a = np.frombuffer(fr, np.uint8)
+    out = np.zeros(n + 1, np.uint8)
+    r = O.model().z1m_decompress(a.ctypes.data, a.size, out.ctypes.data, n)
+    return r, out[: max(r, 0)].tobytes()
+
+
+def gen(rng, n, kind):
+    if kind == 0:
+        return rng.integers(0, 256, n, dtype=np.uint8)
+    if kind == 1:
+        k = int(rng.integers(1, 257))
+        p = rng.dirichlet(np.ones(k) * float(rng.choice([0.05, 0.3, 1, 5])))
+        return rng.choice(k, n, p=p).astype(np.uint8)
+    if kind == 2:
+        vals = rng.integers(0, 256, n // 10 + 2, dtype=np.uint8)
+        lens = rng.geometric(float(rng.choice([0.01, 0.1, 0.5])), n // 10 + 2)
+        return np.repeat(vals, lens)[:n].copy()
+    if kind == 3:
+        return np.where(rng.random(n) < 0.99, 0, rng.integers(0, 256, n)).astype(np.uint8)
+    if kind == 4:
+        b = rng.integers(0, 256, n, dtype=np.uint8)
+        for _ in range(int(rng.integers(0, 100))):
+            if n < 20:
+                break
+            L = int(rng.integers(4, min(n, 3000)))
+            s, d = int(rng.integers(0, n - L + 1)), int(rng.integers(0, n - L + 1))
+            b[d:d + L] = b[s:s + L].copy()
+        return b
+    if kind == 5:
+        p = np.array([2.0 ** -(i + 1) for i in range(40)])
+        return rng.choice(40, n, p=p / p.sum()).astype(np.uint8)
+    return rng.integers(0, int(rng.integers(2, 6)), n, dtype=np.uint8)
+
+
+SIZES = [0, 1, 6, 7, 8, 9, 63, 64, 255, 256, 1023, 1024, 4095, 4096, 16383, 16384, 16385, 65791, 65792,
+         100000, 131072]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_threshold_sizes(n):
+    rng = np.random.default_rng(n)
+    for kind in range(7):
+        b = np.ascontiguousarray(gen(rng, n, kind), dtype=np.uint8)
+        ref = O.zstd_compress1(b)
+        assert model_compress(b) == ref, (n, kind)
+        r, d = model_decompress(ref, b.size)
+        assert r == b.size and d == b.tobytes(), (n, kind)
+
+
+def test_random_fuzz_bounded():
+    rng = np.random.default_rng(12345)
+    t0, cnt = time.time(), 0
+    while time.time() - t0 < 20:
+        n = int(rng.choice([rng.integers(0, 300), rng.integers(0, 20000), rng.integers(0, 131073)]))
+        kind = int(rng.integers(0, 7))
+        b = np.ascontiguousarray(gen(rng, n, kind), dtype=np.uint8)
+        ref = O.zstd_compress1(b)
+        assert model_compress(b) == ref, (n, kind, cnt)
+        cnt += 1
+    assert cnt > 100
+
+
+def test_real_c5_streams():
+    """The five streams of every real POD5 chunk."""
+    from _golden import real_vbz_chunks
+
+    for vbz, n in real_vbz_chunks():
+        _, x = O.vbz_decompress(vbz, n)
+        keys = np.zeros(n // 4 + 1, np.uint8)
+        S, M, Ll, Lh = (np.zeros(n + 1, np.uint8) for _ in range(4))
+        sizes = np.zeros(5, np.uint64)
+        O.oracle().pgno_c5_split(x.ctypes.data, n, keys.ctypes.data, S.ctypes.data, M.ctypes.data,
+                                 Ll.ctypes.data, Lh.ctypes.data, sizes.ctypes.data)
+        for arr, sz in zip((keys, S, M, Ll, Lh), sizes):
+            s = np.ascontiguousarray(arr[: int(sz)])
+            assert model_compress(s) == O.zstd_compress1(s)
