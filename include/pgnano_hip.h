@@ -100,6 +100,10 @@ int pgn_synth_reads_device(pgn_ctx *ctx, size_t nreads, uint64_t seed, uint64_t 
                            const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts,
                            uint32_t p_switch_q16, int32_t level_mean, int32_t level_sd, int32_t noise_sd, void *stream);
 
+/* Diagnostics: accumulated shader-clock cycles per kernel phase (out[0..15] encode, out[16..31]
+ * decode; all zero unless the context was created with PGN_PHASE_PROFILE=1 in the environment). */
+int pgn_debug_phase_cycles(pgn_ctx *ctx, uint64_t *out, int n);
+
 /* Kernel time (ms, HIP events on the launch stream) of the last batch encode / decode call on ctx. */
 float pgn_ctx_last_encode_ms(pgn_ctx *ctx);
 float pgn_ctx_last_decode_ms(pgn_ctx *ctx);

@@ -86,6 +86,7 @@ struct EncArgs {
     uint8_t* scratch;
     size_t slotBytes;
     uint32_t* epochs;
+    uint64_t* prof;
 };
 
 __global__ __launch_bounds__(64) void c5_encode_kernel(EncArgs a)
@@ -111,6 +112,8 @@ __global__ __launch_bounds__(64) void c5_encode_kernel(EncArgs a)
     S.maxSeq = kMaxEncSeq;
     uint8_t* frameTmp = base + lay.frameTmp;
     uint32_t epoch = a.epochs[blockIdx.x];
+    PhaseProf P;
+    P.init(a.prof);
 
     for (size_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
         const uint32_t n = a.sampleCounts[c];
@@ -121,8 +124,9 @@ __global__ __launch_bounds__(64) void c5_encode_kernel(EncArgs a)
             continue;
         }
         uint32_t sizes[5];
-        c5_split_wave(a.samples + a.sampleOffsets[c], n, st, sizes, L.nib);
+        c5_split_wave(a.samples + a.sampleOffsets[c], n, st, sizes, L.split);
         wave_sync();
+        P.mark(0);
         uint64_t off = 0, fsz[5];
         bool overflow = false;
         for (int s = 0; s < 5; s++) {
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(64) void c5_encode_kernel(EncArgs a)
             const uint64_t hdr = (s < 4) ? 8 : 0;
             const bool direct = !overflow && (off + hdr + z1::compress_bound(sizes[s]) <= cap);
             uint8_t* fdst = direct ? dst + off + hdr : frameTmp;
-            fsz[s] = zstd1_compress_wave(fdst, streams[s], sizes[s], L, S, epoch);
+            fsz[s] = zstd1_compress_wave(fdst, streams[s], sizes[s], L, S, epoch, P);
             if (!direct) {
                 if (!overflow && off + hdr + fsz[s] <= cap) wave_copy(dst + off + hdr, frameTmp, fsz[s]);
                 else overflow = true;
@@ -155,6 +159,7 @@ __global__ __launch_bounds__(64) void c5_encode_kernel(EncArgs a)
         }
     }
     if (lane == 0) a.epochs[blockIdx.x] = epoch;
+    P.flush();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -171,10 +176,11 @@ struct DecArgs {
     int32_t* status;
     uint8_t* scratch;
     size_t slotBytes;
+    uint64_t* prof;
 };
 
-__device__ inline int c5_decode_chunk(const uint8_t* src, uint64_t len, int16_t* out, uint32_t n, DecLds& L,
-                                      const DecScratch& S, uint8_t* inter)
+__device__ inline int c5_decode_chunk(const uint8_t* src, uint64_t len, int16_t* out, uint32_t n,
+                                      const DecScratch& S, uint8_t* inter, PhaseProf& P)
 {
     const uint8_t* fp[5];
     uint64_t fl[5], cs[5];
@@ -201,21 +207,23 @@ __device__ inline int c5_decode_chunk(const uint8_t* src, uint64_t len, int16_t*
     }
     uint64_t off = 0, dres[5];
     for (int s = 0; s < 5; s++) {
-        long r = zstd_decompress_wave(fp[s], (size_t)fl[s], inter + off, (size_t)cs[s], L, S);
+        long r = zstd_decompress_wave(fp[s], (size_t)fl[s], inter + off, (size_t)cs[s], S, P);
         if (r < 0) return PGN_ERR_ZSTD_DECOMPRESS;
         dres[s] = (uint64_t)r;
         off += cs[s];
     }
     wave_sync();
+    P.mark(0);
     uint64_t consumed = 0;
-    if (c5_merge_wave(inter, total, dres[1], dres[2], dres[3], out, n, &consumed)) return PGN_ERR_CORRUPT;
+    const int bad = c5_merge_wave(inter, total, dres[1], dres[2], dres[3], out, n, &consumed);
+    P.mark(6);
+    if (bad) return PGN_ERR_CORRUPT;
     if (consumed != total) return PGN_ERR_REMAINING;
     return PGN_OK;
 }
 
 __global__ __launch_bounds__(64) void c5_decode_kernel(DecArgs a)
 {
-    __shared__ DecLds L;
     const DecLayout lay = dec_layout();
     uint8_t* base = a.scratch + (size_t)blockIdx.x * a.slotBytes;
     DecScratch S;
@@ -224,12 +232,15 @@ __global__ __launch_bounds__(64) void c5_decode_kernel(DecArgs a)
     S.maxSeq = kMaxDecSeq;
     S.tables = (z1::FseDTable*)(base + lay.tables);
     uint8_t* inter = base + lay.inter;
+    PhaseProf P;
+    P.init(a.prof);
     for (size_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
         int st = c5_decode_chunk(a.in + a.inOffsets[c], a.inSizes[c], a.samples + a.sampleOffsets[c],
-                                 a.sampleCounts[c], L, S, inter);
+                                 a.sampleCounts[c], S, inter, P);
         if (lane_id() == 0) a.status[c] = st;
         wave_sync();
     }
+    P.flush();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -323,6 +334,7 @@ struct pgn_ctx {
     uint8_t* stage = nullptr;
     size_t stageBytes = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint64_t* prof = nullptr;  // [2][kPhases] phase cycles (encode, decode) when PGN_PHASE_PROFILE=1
     bool encTimed = false, decTimed = false;
     std::mutex mu;
 };
@@ -388,6 +400,12 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     c->encSlotsMax = (size_t)c->numCUs * (size_t)(encPerCU > 16 ? 16 : encPerCU);
     c->decSlotsMax = (size_t)c->numCUs * (size_t)(decPerCU > 16 ? 16 : decPerCU);
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const char* pe = getenv("PGN_PHASE_PROFILE");
+    if (pe && pe[0] == '1') {
+        HIPCHK(hipMalloc(&c->prof, 2 * kPhases * sizeof(uint64_t)));
+        HIPCHK(hipMemset(c->prof, 0, 2 * kPhases * sizeof(uint64_t)));
+        HIPCHK(hipDeviceSynchronize());
+    }
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
     *out = c;
     return PGN_OK;
@@ -402,6 +420,7 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->epochs);
     (void)hipFree(c->decScratch);
     (void)hipFree(c->stage);
+    (void)hipFree(c->prof);
     for (int i = 0; i < 4; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -465,6 +484,7 @@ static int launch_encode(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, c
     a.scratch = c->encScratch;
     a.slotBytes = enc_layout().bytes;
     a.epochs = c->epochs;
+    a.prof = c->prof;
     HIPCHK(hipEventRecord(c->ev[0], s));
     hipLaunchKernelGGL(c5_encode_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
     HIPCHK(hipGetLastError());
@@ -493,6 +513,7 @@ static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const 
     a.status = d_status;
     a.scratch = c->decScratch;
     a.slotBytes = dec_layout().bytes;
+    a.prof = c->prof ? c->prof + kPhases : nullptr;
     HIPCHK(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(c5_decode_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
     HIPCHK(hipGetLastError());
@@ -525,6 +546,19 @@ int pgn_decompress_batch_device(pgn_ctx* c, size_t nchunks, const uint8_t* d_in,
     std::lock_guard<std::mutex> g(c->mu);
     return launch_decode(c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets, d_sample_counts,
                          d_status, stream);
+}
+
+int pgn_debug_phase_cycles(pgn_ctx* c, uint64_t* out, int n)
+{
+    if (!c || !out || n < 2 * kPhases) return PGN_ERR_INVALID_ARG;
+    if (!c->prof) {
+        memset(out, 0, sizeof(uint64_t) * 2 * kPhases);
+        return PGN_OK;
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, c->prof, sizeof(uint64_t) * 2 * kPhases, hipMemcpyDeviceToHost));
+    return PGN_OK;
 }
 
 float pgn_ctx_last_encode_ms(pgn_ctx* c)

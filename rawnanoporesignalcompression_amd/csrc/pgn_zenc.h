@@ -8,6 +8,7 @@
 //   * Huffman bit packing (prefix sum of code lengths, LDS window, byte flush).
 // Serial stages (tree build, weight FSE, sequence FSE) run on lane 0 with the shared zstd1_* code.
 #pragma once
+#include "pgn_c5.h"
 #include "pgn_wave.h"
 #include "zstd1_model.h"
 
@@ -27,7 +28,7 @@ struct EncLds {
     z1::FseCTable fct;
     uint8_t fscratch[64];
     uint32_t win[kWinWords];
-    uint8_t nib[272];
+    SplitLds split;
     uint32_t u[8];
 };
 
@@ -55,7 +56,7 @@ __device__ inline uint32_t wave_match_count(const uint8_t* src, uint32_t a, uint
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             uint32_t o = 4u * (uint32_t)lane + (uint32_t)j;
-            if (o < len && mism == 0xFFFFFFFFu && src[a + n + o] != src[b + n + o]) mism = o;
+            if (o < len && mism == 0xFFFFFFFFu && gb(src + a + n + o) != gb(src + b + n + o)) mism = o;
         }
         bool over = (4u * (uint32_t)lane + 4u > len);
         uint64_t mm = ballot(mism != 0xFFFFFFFFu);
@@ -71,7 +72,15 @@ __device__ inline uint32_t wave_match_count(const uint8_t* src, uint32_t a, uint
 
 __device__ inline uint32_t tagged(uint32_t tag, uint32_t idx) { return (tag << 17) | idx; }
 
-__device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uint32_t n, const z1::Params& p,
+// ZSTD_hashPtr (mls 5 / 6) over 8 global bytes
+__device__ __forceinline__ uint32_t hash_g(const uint8_t* p, unsigned hlog, unsigned mls)
+{
+    const uint64_t v = ld64u(p);
+    if (mls == 5) return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - hlog));
+    return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - hlog));
+}
+
+__device__ __noinline__ uint32_t fast_search_wave(const uint8_t* __restrict__ src, uint32_t n, const z1::Params& p,
                                             uint32_t* __restrict__ ht, uint32_t tag, z1::Seq* __restrict__ seqs,
                                             uint32_t* lastLL)
 {
@@ -92,10 +101,10 @@ __device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uin
         const bool valid = (pk + 1 < ilimit);
         uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu, t0 = 0, t1 = 0;
         if (valid) {
-            h0 = z1::hash_at(src + pk, hlog, mls);
-            h1 = z1::hash_at(src + pk + 1, hlog, mls);
-            t0 = ht[h0];
-            t1 = ht[h1];
+            h0 = hash_g(src + pk, hlog, mls);
+            h1 = hash_g(src + pk + 1, hlog, mls);
+            t0 = gld<uint32_t>(ht + h0);
+            t1 = gld<uint32_t>(ht + h1);
         }
         // most recent in-step writer before me, first in-step writer after me
         uint32_t m0 = 0, m1 = 0;
@@ -128,8 +137,8 @@ __device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uin
         if (valid && lane <= lastCommit) {
             const bool w1 = later1 > lastCommit;
             const bool w0 = (later0 > lastCommit) && (h0 != h1);
-            if (w0) ht[h0] = tagged(tag, (uint32_t)pk + 1);
-            if (w1) ht[h1] = tagged(tag, (uint32_t)pk + 2);
+            if (w0) gst<uint32_t>(ht + h0, tagged(tag, (uint32_t)pk + 1));
+            if (w1) gst<uint32_t>(ht + h1, tagged(tag, (uint32_t)pk + 2));
         }
         if (!hits) {
             wave_sync();
@@ -145,7 +154,7 @@ __device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uin
         uint32_t mLength, offcode;
         if (repf) {
             const long ip2 = ipf + 2;
-            mLength = (src[ip2 - 1] == src[ip2 - (long)off1 - 1]) ? 1u : 0u;
+            mLength = (gb(src + (ip2 - 1)) == gb(src + (ip2 - (long)off1 - 1))) ? 1u : 0u;
             ipm = ip2 - (long)mLength;
             match0 = ipm - (long)off1;
             mLength += 4;
@@ -157,7 +166,7 @@ __device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uin
             off1 = (uint32_t)(ipm - match0);
             offcode = off1 + 2;
             mLength = 4;
-            while ((ipm > anchor) && (match0 > 0) && (src[ipm - 1] == src[match0 - 1])) { ipm--; match0--; mLength++; }
+            while ((ipm > anchor) && (match0 > 0) && (gb(src + (ipm - 1)) == gb(src + (match0 - 1)))) { ipm--; match0--; mLength++; }
         }
         mLength += wave_match_count(src, (uint32_t)ipm + mLength, (uint32_t)match0 + mLength, (uint32_t)iend);
         if (lane == 0) {
@@ -170,15 +179,15 @@ __device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uin
         anchor = ip0;
         if (ip0 <= ilimit) {
             if (lane == 0) {
-                ht[z1::hash_at(src + cur0 + 1, hlog, mls)] = tagged(tag, cur0 + 2);
-                ht[z1::hash_at(src + ip0 - 2, hlog, mls)] = tagged(tag, (uint32_t)(ip0 - 2) + 1);
+                ht[hash_g(src + cur0 + 1, hlog, mls)] = tagged(tag, cur0 + 2);
+                ht[hash_g(src + ip0 - 2, hlog, mls)] = tagged(tag, (uint32_t)(ip0 - 2) + 1);
             }
             if (off2 > 0) {
                 while ((ip0 <= ilimit) && (ld32u(src + ip0) == ld32u(src + ip0 - off2))) {
                     uint32_t rLength = wave_match_count(src, (uint32_t)ip0 + 4, (uint32_t)ip0 + 4 - off2, (uint32_t)iend) + 4;
                     uint32_t t = off2; off2 = off1; off1 = t;
                     if (lane == 0) {
-                        ht[z1::hash_at(src + ip0, hlog, mls)] = tagged(tag, (uint32_t)ip0 + 1);
+                        ht[hash_g(src + ip0, hlog, mls)] = tagged(tag, (uint32_t)ip0 + 1);
                         seqs[nbSeq].litLength = 0;
                         seqs[nbSeq].offset = 1;
                         seqs[nbSeq].mlBase = rLength - 3;
@@ -199,7 +208,7 @@ __device__ inline uint32_t fast_search_wave(const uint8_t* __restrict__ src, uin
 // Huffman bit packing of one segment: symbols are written last-to-first (HUF_compress1X order), so
 // the stream position of a symbol is the sum of the code lengths of the symbols after it.
 // ---------------------------------------------------------------------------------------------
-__device__ inline void huf_encode_segment_wave(uint8_t* __restrict__ out, const uint8_t* __restrict__ src, uint32_t len,
+__device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, const uint8_t* __restrict__ src, uint32_t len,
                                                uint32_t totalBits, const uint32_t* cw, uint32_t* win)
 {
     const int lane = lane_id();
@@ -216,7 +225,7 @@ __device__ inline void huf_encode_segment_wave(uint8_t* __restrict__ out, const 
             nb[j] = 0;
             code[j] = 0;
             if (r < len) {
-                uint32_t c = cw[src[len - 1 - r]];
+                uint32_t c = cw[gb(src + len - 1 - r)];
                 code[j] = c & 0xFFFF;
                 nb[j] = c >> 16;
             }
@@ -247,10 +256,7 @@ __device__ inline void huf_encode_segment_wave(uint8_t* __restrict__ out, const 
         const uint32_t endRel = bitBase + stepBits - winLo;
         const uint32_t complete = endRel >> 5;
         uint8_t* o = out + (winLo >> 3);
-        for (uint32_t w = (uint32_t)lane; w < complete; w += 64) {
-            uint32_t v = win[w];
-            __builtin_memcpy(o + 4 * w, &v, 4);
-        }
+        for (uint32_t w = (uint32_t)lane; w < complete; w += 64) gst<uint32_t>(o + 4 * w, win[w]);
         const uint32_t carry = win[complete];
         wave_sync();
         for (uint32_t w = (uint32_t)lane; w <= complete + 3 && w < (uint32_t)kWinWords; w += 64) win[w] = 0;
@@ -266,9 +272,27 @@ __device__ inline void huf_encode_segment_wave(uint8_t* __restrict__ out, const 
         win[rel >> 5] |= 1u << (rel & 31);
         uint32_t nbytes = ((totalBits + 8) >> 3) - (winLo >> 3);
         uint8_t* o = out + (winLo >> 3);
-        for (uint32_t b = 0; b < nbytes; b++) o[b] = (uint8_t)(win[b >> 2] >> (8 * (b & 3)));
+        for (uint32_t b = 0; b < nbytes; b++) gst<uint8_t>(o + b, (uint8_t)(win[b >> 2] >> (8 * (b & 3))));
     }
     wave_sync();
+}
+
+// lane 0: HUF_buildCTable (from the sorted nodes) + HUF_writeCTable into L.hdr
+__device__ __noinline__ void huf_tree_lane0(EncLds& L, unsigned maxSym, unsigned huffLog)
+{
+    unsigned hl = z1::huf_build_from_sorted(L.nodes, maxSym, huffLog, L.nbBits, L.val);
+    size_t hSize = z1::huf_write_ctable(L.hdr, L.nbBits, maxSym, hl, L.fct, L.fscratch);
+    L.u[0] = hl;
+    L.u[1] = (uint32_t)hSize;
+}
+
+// lane 0: the sequences section into the staging buffer (rare on nanopore streams)
+__device__ __noinline__ void seq_section_lane0(EncLds& L, const EncScratch& S, uint32_t nbSeq)
+{
+    size_t r = z1::compress_sequences(S.seqSection, S.seqs, nbSeq, S.codes, S.codes + S.maxSeq, S.codes + 2 * S.maxSeq,
+                                      *S.seqWork);
+    L.u[2] = (uint32_t)r;
+    L.u[3] = (r == (size_t)-1 || r == (size_t)-2) ? 1u : 0u;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -282,11 +306,11 @@ __device__ inline size_t write_raw_literals_wave(uint8_t* dst, const uint8_t* li
     return fl + n;
 }
 
-__device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
-                                                EncLds& L)
+__device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
+                                                EncLds& L, PhaseProf& P)
 {
     const int lane = lane_id();
-    if (n <= 63) return write_raw_literals_wave(dst, lit, n);
+    if (n <= 63) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     const uint32_t minGain = (n >> 6) + 2;
     const uint32_t lhSize = (uint32_t)z1::huf_lit_header_size(n);
     const bool single = n < 256;
@@ -298,11 +322,10 @@ __device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const
     for (uint32_t i = (uint32_t)lane * 16; i < n; i += 1024) {
         uint8_t b[16];
         if (i + 16 <= n) {
-            uint4 v;
-            __builtin_memcpy(&v, lit + i, 16);
+            const uint4 v = gld<uint4>(lit + i);
             __builtin_memcpy(b, &v, 16);
         } else {
-            for (int k = 0; k < 16; k++) b[k] = (i + k < n) ? lit[i + k] : 0;
+            for (int k = 0; k < 16; k++) b[k] = (i + k < n) ? gb(lit + i + k) : 0;
         }
         uint32_t sa = i / segSize;
         uint32_t boundary = (sa + 1) * segSize;
@@ -328,6 +351,7 @@ __device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const
     const uint32_t maxSym = wave_max(myMaxSym);
     const uint32_t largest = wave_max(myLargest);
     wave_sync();
+    P.mark(3);
     if (largest == n) {  // one symbol: RLE literals
         size_t fl = z1::raw_lit_header_size(n);
         if (lane == 0) {
@@ -336,7 +360,7 @@ __device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const
         }
         return fl + 1;
     }
-    if (largest <= (n >> 7) + 4) return write_raw_literals_wave(dst, lit, n);
+    if (largest <= (n >> 7) + 4) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     unsigned huffLog = z1::huf_optimal_table_log(z1::kHufTableLogDefault, n, maxSym);
     // HUF_sort: rank = #greater + #equal-with-smaller-symbol (stable, decreasing count)
     for (int i = lane; i < 2 * 256 + 4; i += 64) {
@@ -360,15 +384,12 @@ __device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const
         }
     }
     wave_sync();
-    if (lane == 0) {
-        unsigned hl = z1::huf_build_from_sorted(L.nodes, maxSym, huffLog, L.nbBits, L.val);
-        size_t hSize = z1::huf_write_ctable(L.hdr, L.nbBits, maxSym, hl, L.fct, L.fscratch);
-        L.u[0] = hl;
-        L.u[1] = (uint32_t)hSize;
-    }
+    P.mark(4);
+    if (lane == 0) huf_tree_lane0(L, maxSym, huffLog);
     wave_sync();
+    P.mark(5);
     const uint32_t hSize = L.u[1];
-    if (hSize == 0 || hSize + 12 >= n) return write_raw_literals_wave(dst, lit, n);
+    if (hSize == 0 || hSize + 12 >= n) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     // exact stream sizes from the segment histograms
     uint32_t bytes[4] = {0, 0, 0, 0}, bits[4] = {0, 0, 0, 0};
     {
@@ -389,7 +410,7 @@ __device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const
     }
     uint32_t cStreams = single ? bytes[0] : 6 + bytes[0] + bytes[1] + bytes[2] + bytes[3];
     uint32_t total = hSize + cStreams;
-    if (total >= n - 1 || total >= n - minGain) return write_raw_literals_wave(dst, lit, n);
+    if (total >= n - 1 || total >= n - minGain) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     if (lane == 0) {
         z1::write_huf_lit_header(dst, lhSize, n, total, single);
         if (!single) {
@@ -398,7 +419,7 @@ __device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const
             z1::wr16(dst + lhSize + hSize + 4, bytes[2]);
         }
     }
-    for (uint32_t i = (uint32_t)lane; i < hSize; i += 64) dst[lhSize + i] = L.hdr[i];
+    for (uint32_t i = (uint32_t)lane; i < hSize; i += 64) gst<uint8_t>(dst + lhSize + i, L.hdr[i]);
     wave_sync();
     uint8_t* op = dst + lhSize + hSize + (single ? 0 : 6);
     for (int k = 0; k < nseg; k++) {
@@ -407,14 +428,15 @@ __device__ inline size_t compress_literals_wave(uint8_t* __restrict__ dst, const
         huf_encode_segment_wave(op, lit + a, e - a, bits[k], L.cw, L.win);
         op += bytes[k];
     }
+    P.mark(6);
     return lhSize + total;
 }
 
 // ---------------------------------------------------------------------------------------------
 // One stream -> one frame.  dst must have compress_bound(n) bytes.  Returns the frame size.
 // ---------------------------------------------------------------------------------------------
-__device__ inline size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
-                                             EncLds& L, const EncScratch& S, uint32_t tag)
+__device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
+                                             EncLds& L, const EncScratch& S, uint32_t tag, PhaseProf& P)
 {
     const int lane = lane_id();
     if (n == 0) {
@@ -429,6 +451,7 @@ __device__ inline size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const ui
     const z1::Params p = z1::level1_params(n);
     uint32_t lastLL = 0;
     const uint32_t nbSeq = fast_search_wave(src, n, p, S.ht, tag, S.seqs, &lastLL);
+    P.mark(1);
     const uint8_t* lit = src;
     uint32_t nLit = n;
     if (nbSeq > 0) {
@@ -445,23 +468,20 @@ __device__ inline size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const ui
         wave_sync();
         lit = S.lit;
         nLit = o;
+        P.mark(2);
     }
     uint8_t* body = dst + h + 3;
-    const size_t litSize = compress_literals_wave(body, lit, nLit, L);
+    const size_t litSize = compress_literals_wave(body, lit, nLit, L, P);
     wave_sync();
     size_t seqSize;
     if (nbSeq == 0) {
         if (lane == 0) body[litSize] = 0;
         seqSize = 1;
     } else {
-        if (lane == 0) {
-            size_t r = z1::compress_sequences(S.seqSection, S.seqs, nbSeq, S.codes, S.codes + S.maxSeq,
-                                              S.codes + 2 * S.maxSeq, *S.seqWork);
-            L.u[2] = (uint32_t)r;
-            L.u[3] = (r == (size_t)-1 || r == (size_t)-2) ? 1u : 0u;
-        }
+        if (lane == 0) seq_section_lane0(L, S, nbSeq);
         wave_sync();
         seqSize = L.u[3] ? (size_t)-1 : (size_t)L.u[2];
+        P.mark(8);
     }
     const size_t maxCSize = n - ((n >> 6) + 2);
     if (seqSize == (size_t)-1 || litSize + seqSize >= maxCSize) {
@@ -472,6 +492,7 @@ __device__ inline size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const ui
         }
         wave_copy(dst + h + 3, src, n);
         wave_sync();
+        P.mark(9);
         return h + 3 + n;
     }
     if (nbSeq > 0) wave_copy(body + litSize, S.seqSection, seqSize);
@@ -481,6 +502,7 @@ __device__ inline size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const ui
         z1::wr24(dst + h, (uint32_t)(1u + (z1::kBtCompressed << 1) + (cSize << 3)));
     }
     wave_sync();
+    P.mark(9);
     return h + 3 + cSize;
 }
 

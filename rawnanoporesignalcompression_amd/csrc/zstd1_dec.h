@@ -261,11 +261,12 @@ struct HufDTable {
     HufDEntry e[1 << kHufTableLogMax];
 };
 
-// HUF_readStats + HUF_readDTableX1.  Returns header bytes consumed, 0 on error.
-PGN_HD size_t huf_read_dtable(HufDTable& dt, const uint8_t* src, size_t srcSize, FseDTable& scratchDt)
+// HUF_readStats: the weight list of a Huffman table description (direct 4-bit or FSE-compressed).
+// Writes nbW weights (the implied last weight is NOT added).  Returns header bytes consumed, 0 on
+// error.
+PGN_HD size_t huf_read_weights(uint8_t* weights, unsigned* nbWOut, const uint8_t* src, size_t srcSize, FseDTable& scratchDt)
 {
     if (srcSize < 1) return 0;
-    uint8_t weights[256];
     unsigned nbW;
     size_t iSize = src[0];
     size_t used;
@@ -280,7 +281,6 @@ PGN_HD size_t huf_read_dtable(HufDTable& dt, const uint8_t* src, size_t srcSize,
         used = bytes + 1;
     } else {
         if (iSize + 1 > srcSize) return 0;
-        // FSE-compressed weights, max tableLog 6
         int16_t norm[kHufTableLogMax + 1];
         unsigned maxSV = kHufTableLogMax, tl = 0;
         size_t nc = fse_read_ncount(norm, &maxSV, &tl, src + 1, iSize, 6);
@@ -293,19 +293,26 @@ PGN_HD size_t huf_read_dtable(HufDTable& dt, const uint8_t* src, size_t srcSize,
         // alternate states; stop when the stream overruns (FSE_decompress_usingDTable tail rule)
         while (true) {
             if (nbW > 253) return 0;
-            const FseDEntry& e1 = scratchDt.e[st1];
+            const FseDEntry e1 = scratchDt.e[st1];
             weights[nbW++] = e1.symbol;
             st1 = e1.newState + br_read(br, e1.nbBits);
             if (br.pos < 0) { weights[nbW++] = scratchDt.e[st2].symbol; break; }
             if (nbW > 253) return 0;
-            const FseDEntry& e2 = scratchDt.e[st2];
+            const FseDEntry e2 = scratchDt.e[st2];
             weights[nbW++] = e2.symbol;
             st2 = e2.newState + br_read(br, e2.nbBits);
             if (br.pos < 0) { weights[nbW++] = scratchDt.e[st1].symbol; break; }
         }
         used = iSize + 1;
     }
-    // weights -> tableLog, implied last weight
+    *nbWOut = nbW;
+    return used;
+}
+
+// The implied last weight and the table log (HUF_readStats tail).  weights[nbW] receives the last
+// weight; returns the table log, 0 on error.
+PGN_HD unsigned huf_complete_weights(uint8_t* weights, unsigned nbW)
+{
     uint32_t rankStats[kHufTableLogMax + 2];
     for (unsigned i = 0; i < kHufTableLogMax + 2; i++) rankStats[i] = 0;
     uint32_t weightTotal = 0;
@@ -325,7 +332,22 @@ PGN_HD size_t huf_read_dtable(HufDTable& dt, const uint8_t* src, size_t srcSize,
     weights[nbW] = (uint8_t)lastWeight;
     rankStats[lastWeight]++;
     if ((rankStats[1] < 2) || (rankStats[1] & 1)) return 0;
+    return tableLog;
+}
+
+// HUF_readStats + HUF_readDTableX1.  Returns header bytes consumed, 0 on error.
+PGN_HD size_t huf_read_dtable(HufDTable& dt, const uint8_t* src, size_t srcSize, FseDTable& scratchDt)
+{
+    uint8_t weights[256];
+    unsigned nbW = 0;
+    size_t used = huf_read_weights(weights, &nbW, src, srcSize, scratchDt);
+    if (used == 0) return 0;
+    unsigned tableLog = huf_complete_weights(weights, nbW);
+    if (tableLog == 0) return 0;
     unsigned nbSymbols = nbW + 1;
+    uint32_t rankStats[kHufTableLogMax + 2];
+    for (unsigned i = 0; i < kHufTableLogMax + 2; i++) rankStats[i] = 0;
+    for (unsigned n = 0; n < nbSymbols; n++) rankStats[weights[n]]++;
     // fill the table: weight 1 codes first
     uint32_t rankStart[kHufTableLogMax + 2];
     uint32_t next = 0;

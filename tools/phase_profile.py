@@ -1,0 +1,32 @@
+"""Diagnostic: per-phase shader-cycle shares of the encode/decode kernels (PGN_PHASE_PROFILE=1)."""
+import ctypes as C
+import os
+import sys
+
+os.environ["PGN_PHASE_PROFILE"] = "1"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np
+import torch
+
+from rawnanoporesignalcompression_amd import PGNanoCodec
+
+ENC = ["split", "search", "lit_gather", "hist", "sort", "tree+hdr(lane0)", "huf_encode", "raw_lit", "seq(lane0)",
+       "frame_finish"]
+DEC = ["parse/merge_wait", "huf_table(lane0)", "huf_decode", "seq_list(lane0)", "seq_exec", "raw_copy", "merge",
+       "lit_hdr"]
+R = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
+S = 100000
+c = PGNanoCodec(0)
+samples, offs, cnt = c.synth_reads(R, S, seed=42)
+enc = c.compress_batch(samples, offs, cnt)
+out, so, st = c.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
+torch.cuda.synchronize()
+print("encode ms", c.last_encode_ms(), "decode ms", c.last_decode_ms(), "ok", bool(torch.equal(out, samples)))
+buf = np.zeros(32, np.uint64)
+c._lib.pgn_debug_phase_cycles(c._h, buf.ctypes.data, 32)
+for name, lab, arr in (("encode", ENC, buf[:16]), ("decode", DEC, buf[16:])):
+    tot = float(arr.sum())
+    print(f"{name}: total {tot/1e9:.2f} Gcycles (summed over waves), per chunk {tot/R/1e3:.1f} kcycles")
+    for i, l in enumerate(lab):
+        if arr[i]:
+            print(f"   {l:18s} {100*arr[i]/tot:6.2f}%  {arr[i]/R/1e3:9.1f} kcyc/chunk")
