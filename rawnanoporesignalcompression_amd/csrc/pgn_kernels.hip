@@ -22,55 +22,82 @@ constexpr uint32_t kMaxSamples = PGN_MAX_CHUNK_SAMPLES;
 constexpr uint32_t kMaxStream = kMaxSamples;            // largest C5 stream (M/Llow/Lhigh <= n)
 constexpr uint32_t kMaxEncSeq = kMaxStream / 4 + 2;      // every match covers >= 4 bytes
 constexpr uint32_t kMaxDecSeq = kMaxStream / 3 + 2;      // any valid block: matches >= 3 bytes
+constexpr int kStreams = 5;
 
 __host__ __device__ constexpr size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// Capacity of C5 stream s of a chunk of at most kMaxSamples samples: keys n/4, S n/2, M/Ll/Lh n.
+__host__ __device__ constexpr uint32_t stream_cap(int s)
+{
+    return s == 0 ? kMaxSamples / 4 + 1 : (s == 1 ? kMaxSamples / 2 + 1 : kMaxStream);
+}
+__host__ __device__ constexpr size_t stream_pad(int s) { return align_up((size_t)stream_cap(s) + 64, 256); }
+// byte offset of stream s inside a chunk's stream area
+__host__ __device__ constexpr size_t stream_off(int s)
+{
+    size_t o = 0;
+    for (int t = 0; t < s; t++) o += stream_pad(t);
+    return o;
+}
+constexpr size_t kChunkStreamBytes = stream_off(kStreams);
+// ZSTD_COMPRESSBOUND (the frame of a stream never exceeds it)
+__host__ __device__ constexpr size_t frame_bound(size_t n)
+{
+    return n + (n >> 8) + (n < (128u << 10) ? (((128u << 10) - n) >> 11) : 0);
+}
+__host__ __device__ constexpr size_t frame_pad(int s) { return align_up(frame_bound(stream_cap(s)) + 64, 256); }
+__host__ __device__ constexpr size_t frame_off(int s)
+{
+    size_t o = 0;
+    for (int t = 0; t < s; t++) o += frame_pad(t);
+    return o;
+}
+constexpr size_t kChunkFrameBytes = frame_off(kStreams);
+
 // ---------------------------------------------------------------------------------------------
-// Scratch window of one encode slot
+// Scratch of one resident zstd-encode workgroup ("slot")
 // ---------------------------------------------------------------------------------------------
 struct EncLayout {
-    size_t K, S, M, Ll, Lh, ht, lit, seqs, codes, seqSection, seqWork, frameTmp, bytes;
+    size_t ht, lit, seqs, codes, seqSection, seqWork, bytes;
 };
 __host__ __device__ inline EncLayout enc_layout()
 {
     EncLayout l{};
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o = align_up(o + n + 64, 256); return r; };
-    l.K = take(kMaxSamples / 4 + 1);
-    l.S = take(kMaxSamples / 2 + 1);
-    l.M = take(kMaxStream);
-    l.Ll = take(kMaxStream);
-    l.Lh = take(kMaxStream);
     l.ht = take((size_t)4 << 15);
     l.lit = take(kMaxStream);
     l.seqs = take(sizeof(z1::Seq) * kMaxEncSeq);
     l.codes = take(3 * (size_t)kMaxEncSeq);
     l.seqSection = take(16 + 10 * (size_t)kMaxEncSeq + 1024);
     l.seqWork = take(sizeof(z1::SeqWork));
-    l.frameTmp = take(z1::compress_bound(kMaxStream) + 64);
     l.bytes = o;
     return l;
 }
 
 struct DecLayout {
-    size_t inter, lit, seqs, tables, bytes;
+    size_t lit, seqs, tables, bytes;
 };
-constexpr size_t kInterCap = (size_t)5 * kMaxStream;
 __host__ __device__ inline DecLayout dec_layout()
 {
     DecLayout l{};
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o = align_up(o + n + 64, 256); return r; };
-    l.inter = take(kInterCap);
     l.lit = take(kMaxStream);
     l.seqs = take(12 * (size_t)kMaxDecSeq);
     l.tables = take(3 * sizeof(z1::FseDTable));
     l.bytes = o;
     return l;
 }
+constexpr size_t kInterCap = (size_t)5 * kMaxStream;
+constexpr size_t kChunkInterBytes = align_up(kInterCap + 64, 256);
+
+// Work-unit order of the per-stream kernels: the large streams first (M, S, keys, Llow, Lhigh), so
+// the dynamic queue ends with short units.
+__device__ __forceinline__ int unit_stream(uint32_t k) { return (int)((0x43012u >> (4 * k)) & 0xFu); }
 
 // ---------------------------------------------------------------------------------------------
-// Encode
+// Encode: split -> per-stream zstd -> assemble, over a sub-batch of G chunks (chunk g = base + g)
 // ---------------------------------------------------------------------------------------------
 struct EncArgs {
     size_t nchunks;
@@ -83,88 +110,144 @@ struct EncArgs {
     uint64_t* outSizes;
     int32_t* status;
     uint64_t* stats;
-    uint8_t* scratch;
+    uint8_t* streams;    // G * kChunkStreamBytes
+    uint8_t* frames;     // G * kChunkFrameBytes
+    uint32_t* sizes;     // [G][5] raw stream sizes; sizes[g*5] = ~0u marks an unsupported chunk
+    uint32_t* fsizes;    // [G][5] frame sizes
+    uint8_t* slotScratch;
     size_t slotBytes;
     uint32_t* epochs;
+    uint32_t* queue;     // work counter of this sub-batch
     uint64_t* prof;
+    size_t base, G;
 };
 
-__global__ __launch_bounds__(64) void c5_encode_kernel(EncArgs a)
+__global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
 {
-    __shared__ EncLds L;
+    static __shared__ SplitLds W;
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    PhaseProf P;
+    P.init(a.prof);
+    const uint32_t n = a.sampleCounts[c];
+    uint32_t* sz = a.sizes + g * kStreams;
+    if (n > kMaxSamples) {
+        if (lane_id() == 0) {
+            sz[0] = ~0u;
+            a.status[c] = PGN_ERR_UNSUPPORTED;
+            a.outSizes[c] = 0;
+        }
+        return;
+    }
+    uint8_t* base = a.streams + g * kChunkStreamBytes;
+    C5Streams st{base + stream_off(0), base + stream_off(1), base + stream_off(2), base + stream_off(3), base + stream_off(4)};
+    uint32_t sizes[5];
+    c5_split_wave(a.samples + a.sampleOffsets[c], n, st, sizes, W);
+    if (lane_id() == 0)
+        for (int s = 0; s < kStreams; s++) sz[s] = sizes[s];
+    P.mark(0);
+    P.flush();
+}
+
+__global__ __launch_bounds__(64, 16) void enc_zstd_kernel(EncArgs a)
+{
     const int lane = lane_id();
     const EncLayout lay = enc_layout();
-    uint8_t* base = a.scratch + (size_t)blockIdx.x * a.slotBytes;
-    C5Streams st;
-    st.K = base + lay.K;
-    st.S = base + lay.S;
-    st.M = base + lay.M;
-    st.Ll = base + lay.Ll;
-    st.Lh = base + lay.Lh;
-    uint8_t* streams[5] = {st.K, st.S, st.M, st.Ll, st.Lh};
+    uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
     EncScratch S;
-    S.ht = (uint32_t*)(base + lay.ht);
-    S.seqs = (z1::Seq*)(base + lay.seqs);
-    S.codes = base + lay.codes;
-    S.lit = base + lay.lit;
-    S.seqSection = base + lay.seqSection;
-    S.seqWork = (z1::SeqWork*)(base + lay.seqWork);
+    S.ht = (uint32_t*)(sbase + lay.ht);
+    S.seqs = (z1::Seq*)(sbase + lay.seqs);
+    S.codes = sbase + lay.codes;
+    S.lit = sbase + lay.lit;
+    S.seqSection = sbase + lay.seqSection;
+    S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
     S.maxSeq = kMaxEncSeq;
-    uint8_t* frameTmp = base + lay.frameTmp;
     uint32_t epoch = a.epochs[blockIdx.x];
     PhaseProf P;
     P.init(a.prof);
-
-    for (size_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
-        const uint32_t n = a.sampleCounts[c];
-        const uint64_t cap = a.outCaps[c];
-        uint8_t* dst = a.out + a.outOffsets[c];
-        if (n > kMaxSamples) {
-            if (lane == 0) { a.status[c] = PGN_ERR_UNSUPPORTED; a.outSizes[c] = 0; }
-            continue;
-        }
-        uint32_t sizes[5];
-        c5_split_wave(a.samples + a.sampleOffsets[c], n, st, sizes, L.split);
-        wave_sync();
-        P.mark(0);
-        uint64_t off = 0, fsz[5];
-        bool overflow = false;
-        for (int s = 0; s < 5; s++) {
-            if (++epoch >= 32768u) {  // tag space exhausted: clear the table once
-                for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
-                epoch = 1;
-                wave_sync();
-            }
-            const uint64_t hdr = (s < 4) ? 8 : 0;
-            const bool direct = !overflow && (off + hdr + z1::compress_bound(sizes[s]) <= cap);
-            uint8_t* fdst = direct ? dst + off + hdr : frameTmp;
-            fsz[s] = zstd1_compress_wave(fdst, streams[s], sizes[s], L, S, epoch, P);
-            if (!direct) {
-                if (!overflow && off + hdr + fsz[s] <= cap) wave_copy(dst + off + hdr, frameTmp, fsz[s]);
-                else overflow = true;
-            }
-            if (!overflow && hdr && lane == 0) __builtin_memcpy(dst + off, &fsz[s], 8);
-            off += hdr + fsz[s];
+    const size_t G = a.G, units = kStreams * G;
+    while (true) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(a.queue, 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= units) break;
+        const int s = unit_stream((uint32_t)(u / G));
+        const size_t g = u % G;
+        if (a.base + g >= a.nchunks) continue;
+        const uint32_t n = a.sizes[g * kStreams + s];
+        if (a.sizes[g * kStreams] == ~0u) continue;  // unsupported chunk
+        if (++epoch >= 32768u) {  // tag space exhausted: clear the table once
+            for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
+            epoch = 1;
             wave_sync();
         }
-        if (lane == 0) {
-            a.status[c] = overflow ? PGN_ERR_DST_TOO_SMALL : PGN_OK;
-            a.outSizes[c] = off;
-            if (a.stats) {
-                for (int s = 0; s < 5; s++) {
-                    a.stats[c * PGN_STATS_PER_CHUNK + s] = sizes[s];
-                    a.stats[c * PGN_STATS_PER_CHUNK + 5 + s] = fsz[s];
-                }
-            }
-        }
+        const uint8_t* src = a.streams + g * kChunkStreamBytes + stream_off(s);
+        uint8_t* dst = a.frames + g * kChunkFrameBytes + frame_off(s);
+        const size_t fsz = zstd1_compress_wave(dst, src, n, S, epoch, P);
+        if (lane == 0) a.fsizes[g * kStreams + s] = (uint32_t)fsz;
+        wave_sync();
     }
     if (lane == 0) a.epochs[blockIdx.x] = epoch;
     P.flush();
 }
 
+__global__ __launch_bounds__(64) void enc_assemble_kernel(EncArgs a)
+{
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    const int lane = lane_id();
+    const uint32_t* sz = a.sizes + g * kStreams;
+    if (sz[0] == ~0u) return;
+    PhaseProf P;
+    P.init(a.prof);
+    const uint32_t* fs = a.fsizes + g * kStreams;
+    uint64_t total = 0;
+    for (int s = 0; s < kStreams; s++) total += (s < 4 ? 8 : 0) + fs[s];
+    const uint64_t cap = a.outCaps[c];
+    const bool ok = total <= cap;  // C5.hpp:420-427 "Not enough space in destination buffer"
+    if (ok) {
+        uint8_t* dst = a.out + a.outOffsets[c];
+        const uint8_t* fr = a.frames + g * kChunkFrameBytes;
+        uint64_t off = 0;
+        for (int s = 0; s < kStreams; s++) {
+            if (s < 4) {
+                if (lane == 0) {
+                    const uint64_t v = fs[s];
+                    __builtin_memcpy(dst + off, &v, 8);
+                }
+                off += 8;
+            }
+            wave_copy(dst + off, fr + frame_off(s), fs[s]);
+            off += fs[s];
+        }
+    }
+    if (lane == 0) {
+        a.status[c] = ok ? PGN_OK : PGN_ERR_DST_TOO_SMALL;
+        a.outSizes[c] = total;
+        if (a.stats) {
+            for (int s = 0; s < kStreams; s++) {
+                a.stats[c * PGN_STATS_PER_CHUNK + s] = sz[s];
+                a.stats[c * PGN_STATS_PER_CHUNK + 5 + s] = fs[s];
+            }
+        }
+    }
+    P.mark(10);
+    P.flush();
+}
+
 // ---------------------------------------------------------------------------------------------
-// Decode
+// Decode: parse -> per-stream zstd decode -> merge
 // ---------------------------------------------------------------------------------------------
+struct DecUnit {
+    uint64_t src;       // frame offset in the input batch
+    uint32_t len;       // frame bytes
+    uint32_t cs;        // frame content size (= decoded bytes expected)
+    uint32_t interOff;  // offset of this stream in the chunk's intermediate
+    int32_t dres;       // decoded bytes, < 0 on failure
+};
+
 struct DecArgs {
     size_t nchunks;
     const uint8_t* in;
@@ -174,72 +257,110 @@ struct DecArgs {
     const uint64_t* sampleOffsets;
     const uint32_t* sampleCounts;
     int32_t* status;
-    uint8_t* scratch;
+    DecUnit* units;      // [G][5]
+    uint8_t* inter;      // G * kChunkInterBytes
+    uint8_t* slotScratch;
     size_t slotBytes;
+    uint32_t* queue;
     uint64_t* prof;
+    size_t base, G;
 };
 
-__device__ inline int c5_decode_chunk(const uint8_t* src, uint64_t len, int16_t* out, uint32_t n,
-                                      const DecScratch& S, uint8_t* inter, PhaseProf& P)
+// one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
+__device__ inline int c5_parse_chunk(const uint8_t* in, uint64_t src0, uint64_t len, DecUnit* u)
 {
-    const uint8_t* fp[5];
-    uint64_t fl[5], cs[5];
+    const uint8_t* src = in + src0;
     uint64_t pos = 0;
-    for (int s = 0; s < 5; s++) {
+    uint64_t cs[5];
+    for (int s = 0; s < kStreams; s++) {
+        uint64_t fl;
         if (s < 4) {
             if (pos > len || len - pos < 8) return PGN_ERR_CORRUPT;
-            fl[s] = ld64u(src + pos);
+            fl = ld64u(src + pos);
             pos += 8;
-            if (fl[s] > len - pos) return PGN_ERR_CORRUPT;
+            if (fl > len - pos) return PGN_ERR_CORRUPT;
         } else {
-            fl[s] = len - pos;  // last frame length is implicit (C5.hpp:560)
+            fl = len - pos;  // last frame length is implicit (C5.hpp:560)
         }
-        fp[s] = src + pos;
         bool ok = false;
-        cs[s] = z1::frame_content_size(fp[s], (size_t)fl[s], &ok);
+        cs[s] = z1::frame_content_size(src + pos, (size_t)fl, &ok);
         if (!ok) return PGN_ERR_NOT_ZSTD;
-        pos += fl[s];
+        u[s].src = src0 + pos;
+        u[s].len = (uint32_t)fl;
+        pos += fl;
     }
-    uint64_t total = 0;
-    for (int s = 0; s < 5; s++) {
+    uint32_t off = 0;
+    for (int s = 0; s < kStreams; s++) {
         if (cs[s] > kMaxStream) return PGN_ERR_UNSUPPORTED;
-        total += cs[s];
+        u[s].cs = (uint32_t)cs[s];
+        u[s].interOff = off;
+        off += (uint32_t)cs[s];
     }
-    uint64_t off = 0, dres[5];
-    for (int s = 0; s < 5; s++) {
-        long r = zstd_decompress_wave(fp[s], (size_t)fl[s], inter + off, (size_t)cs[s], S, P);
-        if (r < 0) return PGN_ERR_ZSTD_DECOMPRESS;
-        dres[s] = (uint64_t)r;
-        off += cs[s];
-    }
-    wave_sync();
-    P.mark(0);
-    uint64_t consumed = 0;
-    const int bad = c5_merge_wave(inter, total, dres[1], dres[2], dres[3], out, n, &consumed);
-    P.mark(6);
-    if (bad) return PGN_ERR_CORRUPT;
-    if (consumed != total) return PGN_ERR_REMAINING;
     return PGN_OK;
 }
 
-__global__ __launch_bounds__(64) void c5_decode_kernel(DecArgs a)
+__global__ __launch_bounds__(64) void dec_parse_kernel(DecArgs a)
 {
+    const size_t g = (size_t)blockIdx.x * 64 + lane_id();
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    a.status[c] = c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], a.units + g * kStreams);
+}
+
+__global__ __launch_bounds__(64, 16) void dec_zstd_kernel(DecArgs a)
+{
+    const int lane = lane_id();
     const DecLayout lay = dec_layout();
-    uint8_t* base = a.scratch + (size_t)blockIdx.x * a.slotBytes;
+    uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
     DecScratch S;
-    S.lit = base + lay.lit;
-    S.seqs = (uint32_t*)(base + lay.seqs);
+    S.lit = sbase + lay.lit;
+    S.seqs = (uint32_t*)(sbase + lay.seqs);
     S.maxSeq = kMaxDecSeq;
-    S.tables = (z1::FseDTable*)(base + lay.tables);
-    uint8_t* inter = base + lay.inter;
+    S.tables = (z1::FseDTable*)(sbase + lay.tables);
     PhaseProf P;
     P.init(a.prof);
-    for (size_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
-        int st = c5_decode_chunk(a.in + a.inOffsets[c], a.inSizes[c], a.samples + a.sampleOffsets[c],
-                                 a.sampleCounts[c], S, inter, P);
-        if (lane_id() == 0) a.status[c] = st;
+    const size_t G = a.G, units = kStreams * G;
+    while (true) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(a.queue, 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= units) break;
+        const int s = unit_stream((uint32_t)(u / G));
+        const size_t g = u % G;
+        const size_t c = a.base + g;
+        if (c >= a.nchunks || a.status[c] != PGN_OK) continue;
+        DecUnit& d = a.units[g * kStreams + s];
+        const long r = zstd_decompress_wave(a.in + d.src, d.len, a.inter + g * kChunkInterBytes + d.interOff, d.cs, S, P);
+        if (lane == 0) d.dres = (int32_t)r;
         wave_sync();
     }
+    P.flush();
+}
+
+__global__ __launch_bounds__(64) void dec_merge_kernel(DecArgs a)
+{
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    if (a.status[c] != PGN_OK) return;
+    PhaseProf P;
+    P.init(a.prof);
+    const DecUnit* d = a.units + g * kStreams;
+    uint64_t total = 0;
+    int st = PGN_OK;
+    for (int s = 0; s < kStreams; s++) {
+        if (d[s].dres < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
+        total += d[s].cs;
+    }
+    if (st == PGN_OK) {
+        uint64_t consumed = 0;
+        const int bad = c5_merge_wave(a.inter + g * kChunkInterBytes, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres,
+                                      (uint64_t)d[3].dres, a.samples + a.sampleOffsets[c], a.sampleCounts[c], &consumed);
+        if (bad) st = PGN_ERR_CORRUPT;
+        else if (consumed != total) st = PGN_ERR_REMAINING;
+    }
+    if (lane_id() == 0) a.status[c] = st;
+    P.mark(6);
     P.flush();
 }
 
@@ -325,11 +446,20 @@ struct pgn_ctx {
     hipStream_t stream = nullptr;
     int numCUs = 0;
     size_t encSlotsMax = 0, decSlotsMax = 0;
+    size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH)
+    // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
     uint32_t* epochs = nullptr;
+    uint8_t* encChunks = nullptr;  // G * (kChunkStreamBytes + kChunkFrameBytes) + sizes + fsizes
+    size_t encG = 0;
+    // decode
     uint8_t* decScratch = nullptr;
     size_t decSlots = 0;
+    uint8_t* decChunks = nullptr;  // G * kChunkInterBytes + units
+    size_t decG = 0;
+    uint32_t* queues = nullptr;    // one work counter per sub-batch pass
+    size_t nQueues = 0;
     // host-call staging (device buffers)
     uint8_t* stage = nullptr;
     size_t stageBytes = 0;
@@ -393,12 +523,16 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     HIPCHK(hipGetDeviceProperties(&prop, device));
     c->numCUs = prop.multiProcessorCount;
     int encPerCU = 0, decPerCU = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&encPerCU, c5_encode_kernel, 64, 0));
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&decPerCU, c5_decode_kernel, 64, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&encPerCU, enc_zstd_kernel, 64, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&decPerCU, dec_zstd_kernel, 64, 0));
     if (encPerCU < 1) encPerCU = 1;
     if (decPerCU < 1) decPerCU = 1;
     c->encSlotsMax = (size_t)c->numCUs * (size_t)(encPerCU > 16 ? 16 : encPerCU);
     c->decSlotsMax = (size_t)c->numCUs * (size_t)(decPerCU > 16 ? 16 : decPerCU);
+    if (const char* sb = getenv("PGN_SUBBATCH")) {
+        long v = atol(sb);
+        if (v > 0) c->subBatch = (size_t)v;
+    }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     const char* pe = getenv("PGN_PHASE_PROFILE");
     if (pe && pe[0] == '1') {
@@ -419,6 +553,9 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->encScratch);
     (void)hipFree(c->epochs);
     (void)hipFree(c->decScratch);
+    (void)hipFree(c->encChunks);
+    (void)hipFree(c->decChunks);
+    (void)hipFree(c->queues);
     (void)hipFree(c->stage);
     (void)hipFree(c->prof);
     for (int i = 0; i < 4; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
@@ -429,34 +566,65 @@ int pgn_ctx_destroy(pgn_ctx* c)
 
 void* pgn_ctx_stream(pgn_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
-static int ensure_enc(pgn_ctx* c, size_t slots)
+static int ensure_enc(pgn_ctx* c, size_t slots, size_t G)
 {
-    if (slots <= c->encSlots) return PGN_OK;
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->encScratch);
-    (void)hipFree(c->epochs);
-    c->encScratch = nullptr;
-    c->epochs = nullptr;
-    const size_t sb = enc_layout().bytes;
-    HIPCHK(hipMalloc(&c->encScratch, sb * slots));
-    HIPCHK(hipMalloc(&c->epochs, 4 * slots));
-    // tag 0 never matches: a zeroed table is an empty table for every epoch >= 1.  The context
-    // stream is non-blocking, so zero on it and wait before any launch (on any stream) uses it.
-    HIPCHK(hipMemsetAsync(c->epochs, 0, 4 * slots, c->stream));
-    HIPCHK(hipMemsetAsync(c->encScratch, 0, sb * slots, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    c->encSlots = slots;
+    if (slots > c->encSlots) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->encScratch);
+        (void)hipFree(c->epochs);
+        c->encScratch = nullptr;
+        c->epochs = nullptr;
+        const size_t sb = enc_layout().bytes;
+        HIPCHK(hipMalloc(&c->encScratch, sb * slots));
+        HIPCHK(hipMalloc(&c->epochs, 4 * slots));
+        // tag 0 never matches: a zeroed table is an empty table for every epoch >= 1.  The context
+        // stream is non-blocking, so zero on it and wait before any launch (on any stream) uses it.
+        HIPCHK(hipMemsetAsync(c->epochs, 0, 4 * slots, c->stream));
+        HIPCHK(hipMemsetAsync(c->encScratch, 0, sb * slots, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->encSlots = slots;
+    }
+    if (G > c->encG) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->encChunks);
+        c->encChunks = nullptr;
+        HIPCHK(hipMalloc(&c->encChunks, G * (kChunkStreamBytes + kChunkFrameBytes + 2 * 4 * kStreams)));
+        c->encG = G;
+    }
     return PGN_OK;
 }
 
-static int ensure_dec(pgn_ctx* c, size_t slots)
+static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
 {
-    if (slots <= c->decSlots) return PGN_OK;
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(c->decScratch);
-    c->decScratch = nullptr;
-    HIPCHK(hipMalloc(&c->decScratch, dec_layout().bytes * slots));
-    c->decSlots = slots;
+    if (slots > c->decSlots) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->decScratch);
+        c->decScratch = nullptr;
+        HIPCHK(hipMalloc(&c->decScratch, dec_layout().bytes * slots));
+        c->decSlots = slots;
+    }
+    if (G > c->decG) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(c->decChunks);
+        c->decChunks = nullptr;
+        HIPCHK(hipMalloc(&c->decChunks, G * (kChunkInterBytes + kStreams * sizeof(DecUnit))));
+        c->decG = G;
+    }
+    return PGN_OK;
+}
+
+static int ensure_queues(pgn_ctx* c, size_t n, hipStream_t s)
+{
+    if (n > c->nQueues) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(c->queues);
+        c->queues = nullptr;
+        size_t m = n < 64 ? 64 : n;
+        HIPCHK(hipMalloc(&c->queues, 4 * m));
+        c->nQueues = m;
+    }
+    HIPCHK(hipMemsetAsync(c->queues, 0, 4 * n, s));
     return PGN_OK;
 }
 
@@ -467,8 +635,13 @@ static int launch_encode(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, c
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    size_t slots = nchunks < c->encSlotsMax ? nchunks : c->encSlotsMax;
-    int rc = ensure_enc(c, slots);
+    const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
+    const size_t passes = (nchunks + G - 1) / G;
+    const size_t slots = kStreams * G < c->encSlotsMax ? kStreams * G : c->encSlotsMax;
+    int rc = ensure_enc(c, slots, G);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    rc = ensure_queues(c, passes, s);
     if (rc) return rc;
     EncArgs a;
     a.nchunks = nchunks;
@@ -481,12 +654,22 @@ static int launch_encode(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, c
     a.outSizes = d_out_sizes;
     a.status = d_status;
     a.stats = d_stats;
-    a.scratch = c->encScratch;
+    a.streams = c->encChunks;
+    a.frames = c->encChunks + G * kChunkStreamBytes;
+    a.sizes = (uint32_t*)(a.frames + G * kChunkFrameBytes);
+    a.fsizes = a.sizes + G * kStreams;
+    a.slotScratch = c->encScratch;
     a.slotBytes = enc_layout().bytes;
     a.epochs = c->epochs;
     a.prof = c->prof;
-    HIPCHK(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(c5_encode_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+    a.G = G;
+    for (size_t p = 0; p < passes; p++) {
+        a.base = p * G;
+        a.queue = c->queues + p;
+        hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
     c->encTimed = true;
@@ -499,8 +682,13 @@ static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const 
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    size_t slots = nchunks < c->decSlotsMax ? nchunks : c->decSlotsMax;
-    int rc = ensure_dec(c, slots);
+    const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
+    const size_t passes = (nchunks + G - 1) / G;
+    const size_t slots = kStreams * G < c->decSlotsMax ? kStreams * G : c->decSlotsMax;
+    int rc = ensure_dec(c, slots, G);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    rc = ensure_queues(c, passes, s);
     if (rc) return rc;
     DecArgs a;
     a.nchunks = nchunks;
@@ -511,11 +699,19 @@ static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const 
     a.sampleOffsets = d_sample_offsets;
     a.sampleCounts = d_sample_counts;
     a.status = d_status;
-    a.scratch = c->decScratch;
+    a.inter = c->decChunks;
+    a.units = (DecUnit*)(c->decChunks + G * kChunkInterBytes);
+    a.slotScratch = c->decScratch;
     a.slotBytes = dec_layout().bytes;
     a.prof = c->prof ? c->prof + kPhases : nullptr;
-    HIPCHK(hipEventRecord(c->ev[2], s));
-    hipLaunchKernelGGL(c5_decode_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+    a.G = G;
+    for (size_t p = 0; p < passes; p++) {
+        a.base = p * G;
+        a.queue = c->queues + p;
+        hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], s));
     c->decTimed = true;

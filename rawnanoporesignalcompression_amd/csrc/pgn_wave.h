@@ -21,15 +21,56 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l)
 }
 __device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
 
-// inclusive / exclusive prefix sums across the wave
+// Wave-uniform values.  Arguments of a non-inlined device function arrive in VGPRs and are treated
+// as divergent; passing the wave-uniform ones through readfirstlane at entry gives the compiler
+// scalar registers, scalar loop control and scalar address arithmetic back.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int32_t uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni(uint64_t v)
+{
+    return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+__device__ __forceinline__ long uni(long v) { return (long)uni((uint64_t)v); }
+template <class T>
+__device__ __forceinline__ T* uni(T* p)
+{
+    return (T*)uni((uint64_t)p);
+}
+
+// DPP lane moves (GFX9 encodings; gfx950 keeps the row_bcast / wave_shr controls of GFX9).
+// Lanes without a source read 0.
+enum : int {
+    kDppQuadSwap1 = 0xB1,   // quad_perm [1,0,3,2]
+    kDppQuadSwap2 = 0x4E,   // quad_perm [2,3,0,1]
+    kDppRowShr1 = 0x111,
+    kDppRowShr2 = 0x112,
+    kDppRowShr4 = 0x114,
+    kDppRowShr8 = 0x118,
+    kDppWaveShr1 = 0x138,
+    kDppRowBcast15 = 0x142,
+    kDppRowBcast31 = 0x143,
+};
+template <int Ctrl, int RowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, 0xF, true);
+}
+
+// number of set bits of m below this lane
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// inclusive prefix sum across the wave (DPP: 4 in-row steps + 2 row broadcasts)
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x)
 {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t t = __shfl_up(x, d, 64);
-        if (lane >= d) x += t;
-    }
+    x += dpp<kDppRowShr1>(x);
+    x += dpp<kDppRowShr2>(x);
+    x += dpp<kDppRowShr4>(x);
+    x += dpp<kDppRowShr8>(x);
+    x += dpp<kDppRowBcast15, 0xA>(x);
+    x += dpp<kDppRowBcast31, 0xC>(x);
     return x;
 }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return readlane_u32(wave_incl_sum(x), 63); }
@@ -127,12 +168,13 @@ __device__ inline void wave_fill(uint8_t* dst, uint8_t v, size_t n)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Optional phase timers (diagnostic builds of a run: PGN_PHASE_PROFILE=1 in the environment).
-// Shader-clock cycles accumulate per phase in wave-uniform registers; lane 0 adds them to a global
-// buffer at kernel end.  With a null buffer every call is a predictable uniform branch.
+// Optional phase timers, compiled only into the diagnostic build of the library (PGN_PROFILE;
+// `_build/libpgnano_hip_prof.so`, selected with PGN_PHASE_PROFILE=1).  Shader-clock cycles
+// accumulate per phase; lane 0 adds them to a global buffer at kernel end.
 // ---------------------------------------------------------------------------------------------
 constexpr int kPhases = 16;
 struct PhaseProf {
+#ifdef PGN_PROFILE
     uint64_t* out;
     uint64_t last;
     uint64_t acc[kPhases];
@@ -155,6 +197,11 @@ struct PhaseProf {
         if (out && lane_id() == 0)
             for (int i = 0; i < kPhases; i++) atomicAdd((unsigned long long*)&out[i], (unsigned long long)acc[i]);
     }
+#else
+    __device__ __forceinline__ void init(uint64_t*) {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush() {}
+#endif
 };
 
 }  // namespace pgn

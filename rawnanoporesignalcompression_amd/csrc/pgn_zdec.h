@@ -127,6 +127,8 @@ __device__ __forceinline__ uint32_t sb_huf(StgBits& r, int lane, int32_t q, unsi
 __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut)
 {
     const int lane = lane_id();
+    src = uni(src);
+    srcSize = uni((uint64_t)srcSize);
     if (lane == 0) {
         unsigned nbW = 0;
         size_t used = z1::huf_read_weights(sDec.wts, &nbW, src, srcSize, sDec.fscr);
@@ -218,6 +220,11 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
 __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs)
 {
     const int lane = lane_id();
+    tl = uni(tl);
+    hp = uni(hp);
+    remain = uni((uint64_t)remain);
+    dst = uni(dst);
+    rs = uni(rs);
     const int k = lane >> 4, j = lane & 15;
     if (remain < 6) return false;
     const size_t l1 = gld<uint16_t>(hp), l2 = gld<uint16_t>(hp + 2), l3 = gld<uint16_t>(hp + 4);
@@ -437,9 +444,21 @@ __device__ __noinline__ long decode_seq_list(const uint8_t* src, size_t srcSize,
 // Returns the new output position or a negative z1::DecErr.
 __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t seqSize, const uint8_t* lit, size_t rs,
                                                  uint8_t* dst, size_t op, size_t dstCap, size_t frameStart,
-                                                 const DecScratch& S, uint32_t rep[3], bool tvalid[3])
+                                                 DecScratch S, uint32_t rep[3], bool tvalid[3])
 {
     const int lane = lane_id();
+    seqSrc = uni(seqSrc);
+    seqSize = uni((uint64_t)seqSize);
+    lit = uni(lit);
+    rs = uni((uint64_t)rs);
+    dst = uni(dst);
+    op = uni((uint64_t)op);
+    dstCap = uni((uint64_t)dstCap);
+    frameStart = uni((uint64_t)frameStart);
+    S.lit = uni(S.lit);
+    S.seqs = uni(S.seqs);
+    S.maxSeq = uni(S.maxSeq);
+    S.tables = uni(S.tables);
     if (lane == 0) {
         long nb = decode_seq_list(seqSrc, seqSize, S, rep, tvalid);
         sDec.u[1] = (uint32_t)(nb < 0 ? 0xFFFFFFFFu : (uint32_t)nb);
@@ -475,9 +494,17 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
 
 // ZSTD_decompress(dst, dstCap, src, srcSize).  Returns size or a negative z1::DecErr.
 __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ src, size_t srcSize, uint8_t* __restrict__ dst,
-                                            size_t dstCap, const DecScratch& S, PhaseProf& P)
+                                            size_t dstCap, DecScratch S, PhaseProf& P)
 {
     const int lane = lane_id();
+    src = uni(src);
+    srcSize = uni((uint64_t)srcSize);
+    dst = uni(dst);
+    dstCap = uni((uint64_t)dstCap);
+    S.lit = uni(S.lit);
+    S.seqs = uni(S.seqs);
+    S.maxSeq = uni(S.maxSeq);
+    S.tables = uni(S.tables);
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
     while (ip < srcSize) {

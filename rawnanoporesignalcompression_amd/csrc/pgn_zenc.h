@@ -28,9 +28,19 @@ struct EncLds {
     z1::FseCTable fct;
     uint8_t fscratch[64];
     uint32_t win[kWinWords];
-    SplitLds split;
     uint32_t u[8];
+    // Huffman tree workspace
+    uint16_t tanc[256];   // pointer jumping: ancestor of internal node 256 + i
+    uint16_t tdep[256];   //                  distance to it
+    uint32_t rankLast[16];
+    uint32_t vpr[16];     // valPerRank
+    uint32_t wcount[16];  // weight histogram
+    int16_t wnorm[16];
+    uint32_t wcumul[16];
 };
+
+// One instance per encode workgroup (namespace scope, so every access is a DS instruction).
+static __shared__ EncLds sEnc;
 
 struct EncScratch {
     uint32_t* ht;        // 2^15 tagged hash-table entries
@@ -80,12 +90,18 @@ __device__ __forceinline__ uint32_t hash_g(const uint8_t* p, unsigned hlog, unsi
     return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - hlog));
 }
 
-__device__ __noinline__ uint32_t fast_search_wave(const uint8_t* __restrict__ src, uint32_t n, const z1::Params& p,
-                                            uint32_t* __restrict__ ht, uint32_t tag, z1::Seq* __restrict__ seqs,
-                                            uint32_t* lastLL)
+// Returns nbSeq | lastLiterals << 32.
+__device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ src, uint32_t n, unsigned hlog, unsigned mls,
+                                                  uint32_t* __restrict__ ht, uint32_t tag, z1::Seq* __restrict__ seqs)
 {
     const int lane = lane_id();
-    const unsigned hlog = p.hashLog, mls = p.mls;
+    src = uni(src);
+    n = uni(n);
+    hlog = uni(hlog);
+    mls = uni(mls);
+    ht = uni(ht);
+    tag = uni(tag);
+    seqs = uni(seqs);
     const long iend = (long)n, ilimit = (long)n - 8;
     long ip0 = 1, anchor = 0;
     uint32_t off1 = 1, off2 = 0;
@@ -200,8 +216,7 @@ __device__ __noinline__ uint32_t fast_search_wave(const uint8_t* __restrict__ sr
         }
         wave_sync();
     }
-    *lastLL = (uint32_t)(iend - anchor);
-    return nbSeq;
+    return (uint64_t)nbSeq | ((uint64_t)(iend - anchor) << 32);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -209,9 +224,15 @@ __device__ __noinline__ uint32_t fast_search_wave(const uint8_t* __restrict__ sr
 // the stream position of a symbol is the sum of the code lengths of the symbols after it.
 // ---------------------------------------------------------------------------------------------
 __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, const uint8_t* __restrict__ src, uint32_t len,
-                                               uint32_t totalBits, const uint32_t* cw, uint32_t* win)
+                                                     uint32_t totalBits)
 {
     const int lane = lane_id();
+    out = uni(out);
+    src = uni(src);
+    len = uni(len);
+    totalBits = uni(totalBits);
+    const uint32_t* cw = sEnc.cw;
+    uint32_t* win = sEnc.win;
     for (int w = lane; w < kWinWords; w += 64) win[w] = 0;
     wave_sync();
     uint32_t winLo = 0;   // bit offset of win[0] (multiple of 32)
@@ -277,18 +298,391 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
     wave_sync();
 }
 
-// lane 0: HUF_buildCTable (from the sorted nodes) + HUF_writeCTable into L.hdr
-__device__ __noinline__ void huf_tree_lane0(EncLds& L, unsigned maxSym, unsigned huffLog)
+// ---------------------------------------------------------------------------------------------
+// Huffman tree on the wave: HUF_buildCTable_wksp + HUF_setMaxHeight (libzstd 1.4.x) over the sorted
+// leaves L.nodes[1 + r] (count desc, symbol asc; zero past the last symbol).  The two-queue merge
+// runs wave-uniform (scalar control, look-ahead registers for both queue heads); depths come from
+// pointer jumping over the parent links; the rank boundaries of HUF_setMaxHeight and the canonical
+// codes from ballots.  Writes L.nbBits / L.val per symbol; returns the largest code length.
+// nnz = number of symbols with a nonzero count (>= 2).
+// ---------------------------------------------------------------------------------------------
+__device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBits, uint32_t nnz)
 {
-    unsigned hl = z1::huf_build_from_sorted(L.nodes, maxSym, huffLog, L.nbBits, L.val);
-    size_t hSize = z1::huf_write_ctable(L.hdr, L.nbBits, maxSym, hl, L.fct, L.fscratch);
-    L.u[0] = hl;
-    L.u[1] = (uint32_t)hSize;
+    EncLds& L = sEnc;
+    const int lane = lane_id();
+    maxSym = uni(maxSym);
+    maxNbBits = uni(maxNbBits);
+    nnz = uni(nnz);
+    z1::HufNode* hn = L.nodes + 1;
+    constexpr int kStart = z1::kHufStartNode;
+    const int nonNullRank = (int)nnz - 1;
+    const int nodeRoot = kStart + nonNullRank - 1;
+    L.nodes[0].count = 1u << 31;  // huffNode0[0]: barrier below the leaves
+    // ---- create parents (two queues: leaves ascending from lowS down, nodes from lowN up)
+    int lowS = nonNullRank, lowN = kStart, nodeNb = kStart;
+    const uint32_t c0 = hn[lowS].count + hn[lowS - 1].count;
+    hn[nodeNb].count = c0;
+    hn[lowS].parent = (uint16_t)nodeNb;
+    hn[lowS - 1].parent = (uint16_t)nodeNb;
+    nodeNb++;
+    lowS -= 2;
+    uint32_t S0 = lowS >= 0 ? hn[lowS].count : (1u << 31);
+    uint32_t S1 = lowS >= 1 ? hn[lowS - 1].count : (1u << 31);
+    uint32_t Q0 = c0, Q1 = 1u << 30;  // uncreated nodes read 1 << 30, as in the reference
+    while (nodeNb <= nodeRoot) {
+        int nn[2];
+        uint32_t vv[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            if (S0 < Q0) {
+                nn[k] = lowS;
+                vv[k] = S0;
+                lowS--;
+                S0 = S1;
+                S1 = lowS >= 1 ? hn[lowS - 1].count : (1u << 31);
+            } else {
+                nn[k] = lowN;
+                vv[k] = Q0;
+                lowN++;
+                Q0 = Q1;
+                Q1 = (lowN + 1 < nodeNb) ? hn[lowN + 1].count : (1u << 30);
+            }
+        }
+        const uint32_t cn = vv[0] + vv[1];
+        hn[nodeNb].count = cn;
+        hn[nn[0]].parent = (uint16_t)nodeNb;
+        hn[nn[1]].parent = (uint16_t)nodeNb;
+        if (lowN == nodeNb) Q0 = cn;
+        else if (lowN + 1 == nodeNb) Q1 = cn;
+        nodeNb++;
+    }
+    lds_sync();
+    // ---- depths of the internal nodes: pointer jumping (distance to ancestor, ancestor of ancestor)
+    uint32_t anc[4], dep[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int i = kStart + lane + 64 * j;
+        anc[j] = (uint32_t)nodeRoot;
+        dep[j] = 0;
+        if (i < nodeRoot) {
+            anc[j] = hn[i].parent;
+            dep[j] = 1;
+        }
+        L.tanc[lane + 64 * j] = (uint16_t)anc[j];
+        L.tdep[lane + 64 * j] = (uint16_t)dep[j];
+    }
+    lds_sync();
+    while (true) {
+        bool more = false;
+        uint32_t na[4], nd[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            na[j] = anc[j];
+            nd[j] = dep[j];
+            if (anc[j] != (uint32_t)nodeRoot) {
+                nd[j] = dep[j] + L.tdep[anc[j] - kStart];
+                na[j] = L.tanc[anc[j] - kStart];
+                more |= na[j] != (uint32_t)nodeRoot;
+            }
+        }
+        lds_sync();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            anc[j] = na[j];
+            dep[j] = nd[j];
+            L.tanc[lane + 64 * j] = (uint16_t)na[j];
+            L.tdep[lane + 64 * j] = (uint16_t)nd[j];
+        }
+        lds_sync();
+        if (!ballot(more)) break;
+    }
+    // leaves: parent depth + 1
+    uint32_t nbR[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int r = lane + 64 * j;
+        nbR[j] = 0;
+        if (r <= nonNullRank) {
+            nbR[j] = (uint32_t)L.tdep[hn[r].parent - kStart] + 1u;
+            hn[r].nbBits = (uint8_t)nbR[j];
+        }
+    }
+    lds_sync();
+    // ---- HUF_setMaxHeight
+    const uint32_t largestBits = hn[nonNullRank].nbBits;
+    if (largestBits > maxNbBits) {
+        const uint32_t baseCost = 1u << (largestBits - maxNbBits);
+        int cost = 0;
+        uint32_t nLess = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = lane + 64 * j;
+            const bool in = r <= nonNullRank;
+            if (in && nbR[j] > maxNbBits) {
+                cost += (int)(baseCost - (1u << (largestBits - nbR[j])));
+                nbR[j] = maxNbBits;
+                hn[r].nbBits = (uint8_t)maxNbBits;
+            }
+            nLess += (uint32_t)__builtin_popcountll(ballot(in && nbR[j] < maxNbBits));
+        }
+        int totalCost = (int)wave_sum((uint32_t)cost);
+        int n = (int)nLess - 1;  // last rank shorter than maxNbBits (depths grow with rank)
+        totalCost >>= (largestBits - maxNbBits);
+        const uint32_t noSymbol = 0xF0F0F0F0u;
+        if (lane < 16) L.rankLast[lane] = noSymbol;
+        lds_sync();
+        // rankLast[maxNbBits - b] = last rank of length b (the reference's downward scan)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = lane + 64 * j;
+            if (r <= n) {
+                const uint32_t b = nbR[j];
+                const uint32_t bn = (r == n) ? maxNbBits : (uint32_t)hn[r + 1].nbBits;
+                if (b < bn) L.rankLast[maxNbBits - b] = (uint32_t)r;
+            }
+        }
+        lds_sync();
+        while (totalCost > 0) {
+            unsigned nBitsToDecrease = z1::highbit32((uint32_t)totalCost) + 1;
+            for (; nBitsToDecrease > 1; nBitsToDecrease--) {
+                const uint32_t highPos = L.rankLast[nBitsToDecrease];
+                const uint32_t lowPos = L.rankLast[nBitsToDecrease - 1];
+                if (highPos == noSymbol) continue;
+                if (lowPos == noSymbol) break;
+                if (hn[highPos].count <= 2 * hn[lowPos].count) break;
+            }
+            while ((nBitsToDecrease <= z1::kHufTableLogMax) && (L.rankLast[nBitsToDecrease] == noSymbol)) nBitsToDecrease++;
+            totalCost -= 1 << (nBitsToDecrease - 1);
+            if (L.rankLast[nBitsToDecrease - 1] == noSymbol) L.rankLast[nBitsToDecrease - 1] = L.rankLast[nBitsToDecrease];
+            const uint32_t rl = L.rankLast[nBitsToDecrease];
+            hn[rl].nbBits = (uint8_t)(hn[rl].nbBits + 1);
+            if (rl == 0) {
+                L.rankLast[nBitsToDecrease] = noSymbol;
+            } else {
+                L.rankLast[nBitsToDecrease] = rl - 1;
+                if (hn[rl - 1].nbBits != maxNbBits - nBitsToDecrease) L.rankLast[nBitsToDecrease] = noSymbol;
+            }
+            lds_sync();
+        }
+        while (totalCost < 0) {
+            if (L.rankLast[1] == noSymbol) {
+                while (hn[n].nbBits == maxNbBits) n--;
+                hn[n + 1].nbBits = (uint8_t)(hn[n + 1].nbBits - 1);
+                L.rankLast[1] = (uint32_t)(n + 1);
+                totalCost++;
+                lds_sync();
+                continue;
+            }
+            const uint32_t rl = L.rankLast[1] + 1;
+            hn[rl].nbBits = (uint8_t)(hn[rl].nbBits - 1);
+            L.rankLast[1] = rl;
+            totalCost++;
+            lds_sync();
+        }
+        lds_sync();
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = lane + 64 * j;
+            if (r <= nonNullRank) nbR[j] = hn[r].nbBits;
+        }
+    } else {
+        maxNbBits = largestBits;
+    }
+    // ---- canonical codes: starting value per length, then symbol order within a length
+    {
+        uint32_t mn = 0;
+        for (int b = (int)maxNbBits; b > 0; b--) {
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) cnt += (uint32_t)__builtin_popcountll(ballot(nbR[j] == (uint32_t)b));
+            if (lane == 0) L.vpr[b] = mn;
+            mn = (mn + cnt) >> 1;
+        }
+        if (lane == 0) L.vpr[0] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int r = lane + 64 * j;
+        if (r <= (int)maxSym) L.nbBits[hn[r].byte] = hn[r].nbBits;
+    }
+    lds_sync();
+    uint32_t nbS[4], val[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t s = (uint32_t)lane + 64u * (uint32_t)j;
+        nbS[j] = s <= maxSym ? L.nbBits[s] : 0xFFu;
+        val[j] = 0;
+    }
+    for (uint32_t b = 0; b <= maxNbBits; b++) {
+        uint32_t base = L.vpr[b];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t m = ballot(nbS[j] == b);
+            if (nbS[j] == b) val[j] = base + mbcnt(m);
+            base += (uint32_t)__builtin_popcountll(m);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t s = (uint32_t)lane + 64u * (uint32_t)j;
+        if (s <= maxSym) L.val[s] = (uint16_t)val[j];
+    }
+    lds_sync();
+    return maxNbBits;
+}
+
+// FSE_buildCTable_wksp for the weight alphabet (<= 13 symbols, tableLog <= 6), wave-uniform
+__device__ __forceinline__ void fse_build_ctable_small(z1::FseCTable& ct, const int16_t* norm, unsigned maxSymbolValue,
+                                                       unsigned tableLog, uint8_t* tableSymbol, uint32_t* cumul)
+{
+    const uint32_t tableSize = 1u << tableLog;
+    const uint32_t tableMask = tableSize - 1;
+    const uint32_t step = (tableSize >> 1) + (tableSize >> 3) + 3;
+    uint32_t highThreshold = tableSize - 1;
+    ct.tableLog = tableLog;
+    cumul[0] = 0;
+    for (unsigned u = 1; u <= maxSymbolValue + 1; u++) {
+        if (norm[u - 1] == -1) {
+            cumul[u] = cumul[u - 1] + 1;
+            tableSymbol[highThreshold--] = (uint8_t)(u - 1);
+        } else {
+            cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
+        }
+    }
+    cumul[maxSymbolValue + 1] = tableSize + 1;
+    uint32_t position = 0;
+    for (unsigned symbol = 0; symbol <= maxSymbolValue; symbol++) {
+        const int freq = norm[symbol];
+        for (int k = 0; k < freq; k++) {
+            tableSymbol[position] = (uint8_t)symbol;
+            position = (position + step) & tableMask;
+            while (position > highThreshold) position = (position + step) & tableMask;
+        }
+    }
+    lds_sync();
+    for (uint32_t u = 0; u < tableSize; u++) {
+        const uint8_t sy = tableSymbol[u];
+        const uint32_t cs = cumul[sy];
+        ct.stateTable[cs] = (uint16_t)(tableSize + u);
+        cumul[sy] = cs + 1;
+    }
+    unsigned total = 0;
+    for (unsigned sy = 0; sy <= maxSymbolValue; sy++) {
+        const int nv = norm[sy];
+        if (nv == 0) {
+            ct.deltaNbBits[sy] = ((tableLog + 1) << 16) - (1u << tableLog);
+            ct.deltaFindState[sy] = 0;
+        } else if (nv == -1 || nv == 1) {
+            ct.deltaNbBits[sy] = (tableLog << 16) - (1u << tableLog);
+            ct.deltaFindState[sy] = (int32_t)total - 1;
+            total++;
+        } else {
+            const uint32_t maxBitsOut = tableLog - z1::highbit32((uint32_t)(nv - 1));
+            const uint32_t minStatePlus = (uint32_t)nv << maxBitsOut;
+            ct.deltaNbBits[sy] = (maxBitsOut << 16) - minStatePlus;
+            ct.deltaFindState[sy] = (int32_t)total - nv;
+            total += (unsigned)nv;
+        }
+    }
+    lds_sync();
+}
+
+// HUF_writeCTable into L.hdr from L.nbBits (wave-uniform; weights and their histogram by ballots).
+// Returns the description size, 0 if it cannot be written (raw weights with > 128 symbols).
+__device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t huffLog)
+{
+    EncLds& L = sEnc;
+    const int lane = lane_id();
+    maxSym = uni(maxSym);
+    huffLog = uni(huffLog);
+    const uint32_t wtSize = maxSym;  // weights of symbols 0 .. maxSym-1
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t s = (uint32_t)lane + 64u * (uint32_t)j;
+        w[j] = 0xFFu;
+        if (s < wtSize) {
+            const uint32_t nb = L.nbBits[s];
+            w[j] = nb ? huffLog + 1 - nb : 0u;
+            L.weights[s] = (uint8_t)w[j];
+        }
+    }
+    for (uint32_t v = 0; v <= z1::kHufTableLogMax; v++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) c += (uint32_t)__builtin_popcountll(ballot(w[j] == v));
+        if (lane == 0) L.wcount[v] = c;
+    }
+    lds_sync();
+    // HUF_compressWeights
+    uint32_t hSize = 0;
+    if (wtSize > 1) {
+        unsigned maxW = z1::kHufTableLogMax;
+        while (!L.wcount[maxW]) maxW--;
+        uint32_t maxCount = 0;
+        for (unsigned v = 0; v <= maxW; v++) maxCount = L.wcount[v] > maxCount ? L.wcount[v] : maxCount;
+        if (maxCount == wtSize) {
+            hSize = 1;
+        } else if (maxCount > 1) {
+            const unsigned tableLog = z1::fse_optimal_table_log(6, wtSize, maxW, 2);
+            if (z1::fse_normalize(L.wnorm, tableLog, L.wcount, wtSize, maxW, false)) {
+                lds_sync();
+                const size_t nh = z1::fse_write_ncount(L.hdr + 1, L.wnorm, maxW, tableLog);
+                if (nh && wtSize > 2) {
+                    fse_build_ctable_small(L.fct, L.wnorm, maxW, tableLog, L.fscratch, L.wcumul);
+                    uint8_t* op = L.hdr + 1 + nh;
+                    z1::BitW bw;
+                    z1::bw_init(bw, op);
+                    const uint8_t* ip = L.weights + wtSize;
+                    z1::FseState s1, s2;
+                    size_t left = wtSize;
+                    if (left & 1) {
+                        z1::fse_init_state2(s1, L.fct, *--ip);
+                        z1::fse_init_state2(s2, L.fct, *--ip);
+                        z1::fse_encode(bw, s1, L.fct, *--ip);
+                    } else {
+                        z1::fse_init_state2(s2, L.fct, *--ip);
+                        z1::fse_init_state2(s1, L.fct, *--ip);
+                    }
+                    left -= 2;
+                    if (left & 2) {
+                        z1::fse_encode(bw, s2, L.fct, *--ip);
+                        z1::fse_encode(bw, s1, L.fct, *--ip);
+                    }
+                    while (ip > L.weights) {
+                        z1::fse_encode(bw, s2, L.fct, *--ip);
+                        z1::fse_encode(bw, s1, L.fct, *--ip);
+                        z1::fse_encode(bw, s2, L.fct, *--ip);
+                        z1::fse_encode(bw, s1, L.fct, *--ip);
+                    }
+                    z1::fse_flush(bw, s2, L.fct);
+                    z1::fse_flush(bw, s1, L.fct);
+                    hSize = (uint32_t)(nh + z1::bw_close(bw, op));
+                }
+            }
+        }
+    }
+    lds_sync();
+    if (hSize > 1 && hSize < maxSym / 2) {
+        if (lane == 0) L.hdr[0] = (uint8_t)hSize;
+        lds_sync();
+        return hSize + 1;
+    }
+    if (maxSym > 128) return 0;
+    // raw 4-bit weights
+    if (lane == 0) L.hdr[0] = (uint8_t)(128 + (maxSym - 1));
+    if ((uint32_t)lane < (maxSym + 1) / 2) {
+        const uint32_t a = L.weights[2 * lane], b = (2u * (uint32_t)lane + 1u < maxSym) ? L.weights[2 * lane + 1] : 0u;
+        L.hdr[1 + lane] = (uint8_t)((a << 4) + b);
+    }
+    lds_sync();
+    return (maxSym + 1) / 2 + 1;
 }
 
 // lane 0: the sequences section into the staging buffer (rare on nanopore streams)
-__device__ __noinline__ void seq_section_lane0(EncLds& L, const EncScratch& S, uint32_t nbSeq)
+__device__ __noinline__ void seq_section_lane0(EncScratch S, uint32_t nbSeq)
 {
+    EncLds& L = sEnc;
     size_t r = z1::compress_sequences(S.seqSection, S.seqs, nbSeq, S.codes, S.codes + S.maxSeq, S.codes + 2 * S.maxSeq,
                                       *S.seqWork);
     L.u[2] = (uint32_t)r;
@@ -307,8 +701,12 @@ __device__ inline size_t write_raw_literals_wave(uint8_t* dst, const uint8_t* li
 }
 
 __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
-                                                EncLds& L, PhaseProf& P)
+                                                PhaseProf& P)
 {
+    EncLds& L = sEnc;
+    dst = uni(dst);
+    lit = uni(lit);
+    n = uni(n);
     const int lane = lane_id();
     if (n <= 63) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     const uint32_t minGain = (n >> 6) + 2;
@@ -385,10 +783,12 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     }
     wave_sync();
     P.mark(4);
-    if (lane == 0) huf_tree_lane0(L, maxSym, huffLog);
-    wave_sync();
+    uint32_t nnz = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) nnz += (uint32_t)__builtin_popcountll(ballot(c[q] != 0));
+    const uint32_t hl = huf_tree_wave(maxSym, huffLog, nnz);
+    const uint32_t hSize = huf_write_ctable_wave(maxSym, hl);
     P.mark(5);
-    const uint32_t hSize = L.u[1];
     if (hSize == 0 || hSize + 12 >= n) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     // exact stream sizes from the segment histograms
     uint32_t bytes[4] = {0, 0, 0, 0}, bits[4] = {0, 0, 0, 0};
@@ -425,7 +825,7 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     for (int k = 0; k < nseg; k++) {
         uint32_t a = segSize * (uint32_t)k;
         uint32_t e = (k == nseg - 1) ? n : a + segSize;
-        huf_encode_segment_wave(op, lit + a, e - a, bits[k], L.cw, L.win);
+        huf_encode_segment_wave(op, lit + a, e - a, bits[k]);
         op += bytes[k];
     }
     P.mark(6);
@@ -436,8 +836,20 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
 // One stream -> one frame.  dst must have compress_bound(n) bytes.  Returns the frame size.
 // ---------------------------------------------------------------------------------------------
 __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
-                                             EncLds& L, const EncScratch& S, uint32_t tag, PhaseProf& P)
+                                             EncScratch S, uint32_t tag, PhaseProf& P)
 {
+    EncLds& L = sEnc;
+    dst = uni(dst);
+    src = uni(src);
+    n = uni(n);
+    tag = uni(tag);
+    S.ht = uni(S.ht);
+    S.seqs = uni(S.seqs);
+    S.codes = uni(S.codes);
+    S.lit = uni(S.lit);
+    S.seqSection = uni(S.seqSection);
+    S.seqWork = uni(S.seqWork);
+    S.maxSeq = uni(S.maxSeq);
     const int lane = lane_id();
     if (n == 0) {
         if (lane == 0) z1::write_empty_frame(dst);
@@ -449,8 +861,8 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         return h + 3 + n;
     }
     const z1::Params p = z1::level1_params(n);
-    uint32_t lastLL = 0;
-    const uint32_t nbSeq = fast_search_wave(src, n, p, S.ht, tag, S.seqs, &lastLL);
+    const uint64_t sr = fast_search_wave(src, n, p.hashLog, p.mls, S.ht, tag, S.seqs);
+    const uint32_t nbSeq = (uint32_t)sr, lastLL = (uint32_t)(sr >> 32);
     P.mark(1);
     const uint8_t* lit = src;
     uint32_t nLit = n;
@@ -471,14 +883,14 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         P.mark(2);
     }
     uint8_t* body = dst + h + 3;
-    const size_t litSize = compress_literals_wave(body, lit, nLit, L, P);
+    const size_t litSize = compress_literals_wave(body, lit, nLit, P);
     wave_sync();
     size_t seqSize;
     if (nbSeq == 0) {
         if (lane == 0) body[litSize] = 0;
         seqSize = 1;
     } else {
-        if (lane == 0) seq_section_lane0(L, S, nbSeq);
+        if (lane == 0) seq_section_lane0(S, nbSeq);
         wave_sync();
         seqSize = L.u[3] ? (size_t)-1 : (size_t)L.u[2];
         P.mark(8);

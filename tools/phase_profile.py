@@ -3,7 +3,7 @@ import ctypes as C
 import os
 import sys
 
-os.environ["PGN_PHASE_PROFILE"] = "1"
+os.environ.setdefault("PGN_PHASE_PROFILE", "1")
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import numpy as np
 import torch
