@@ -11,6 +11,8 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libpgnano_hip.so")
+# diagnostic build with per-phase shader-clock timers (tools/phase_profile.py)
+PROF_LIB_PATH = os.path.join(_HERE, "_build", "libpgnano_hip_prof.so")
 
 PGN_OK = 0
 PGN_ERR_DST_TOO_SMALL = 1
@@ -65,7 +67,7 @@ def load(path: str | None = None) -> C.CDLL:
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or LIB_PATH
+        p = path or (PROF_LIB_PATH if os.environ.get("PGN_PHASE_PROFILE") == "1" else LIB_PATH)
         # One HIP runtime per process: PyTorch ships its own libamdhip64 (soname libamdhip64.so.7,
         # but its libraries NEED the unversioned name), so load torch first and let this library
         # bind to the runtime torch already mapped; loading ours first would map a second runtime.

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
     P.flush();
 }
 
-__global__ __launch_bounds__(64, 16) void enc_zstd_kernel(EncArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void enc_zstd_kernel(EncArgs a)
 {
     const int lane = lane_id();
     const EncLayout lay = enc_layout();
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(64) void dec_parse_kernel(DecArgs a)
     a.status[c] = c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], a.units + g * kStreams);
 }
 
-__global__ __launch_bounds__(64, 16) void dec_zstd_kernel(DecArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void dec_zstd_kernel(DecArgs a)
 {
     const int lane = lane_id();
     const DecLayout lay = dec_layout();

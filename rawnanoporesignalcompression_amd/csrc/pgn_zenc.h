@@ -15,29 +15,51 @@
 namespace pgn {
 
 constexpr int kWinWords = 200;  // 512 symbols * 12 bits / 32 + carry
+constexpr int kFiltSlots = 1024;  // match-search round filter (64 lanes x 2 hashes)
 
-struct EncLds {
-    uint32_t hist4[4][256];
-    uint32_t count[256];
-    uint32_t cw[256];  // Huffman code | nbBits << 16
-    z1::HufNode nodes[2 * 256 + 4];
-    uint8_t nbBits[256];
-    uint16_t val[256];
-    uint8_t weights[256];
-    uint8_t hdr[320];  // Huffman table description staged before it is known to be used
-    z1::FseCTable fct;
-    uint8_t fscratch[64];
-    uint32_t win[kWinWords];
-    uint32_t u[8];
-    // Huffman tree workspace
-    uint16_t tanc[256];   // pointer jumping: ancestor of internal node 256 + i
-    uint16_t tdep[256];   //                  distance to it
-    uint32_t rankLast[16];
-    uint32_t vpr[16];     // valPerRank
-    uint32_t wcount[16];  // weight histogram
-    int16_t wnorm[16];
-    uint32_t wcumul[16];
+// FSE compression table of the Huffman weight alphabet (<= 13 symbols, tableLog <= 6)
+struct WCTable {
+    uint32_t tableLog;
+    uint16_t stateTable[64];
+    uint32_t deltaNbBits[16];
+    int32_t deltaFindState[16];
 };
+
+// LDS of one encode wave.  The match search and the literal stage never overlap, so their
+// workspaces share storage.
+struct EncLds {
+    union {
+        struct {  // match search: hash-slot filter of the current round (bit per lane), the round's visits
+            uint64_t filt[kFiltSlots];
+            uint32_t vh0[64], vh1[64], vpk[64];
+        };
+        struct {  // literals
+            uint32_t hist2[2][256];  // per-segment histograms, two 16-bit counts per word
+            uint32_t count[256];
+            uint32_t cw[256];  // Huffman code | nbBits << 16
+            z1::HufNode nodes[2 * 256 + 4];
+            uint8_t nbBits[256];
+            uint16_t val[256];
+            uint8_t weights[256];
+            uint8_t hdr[256];  // Huffman table description (the FSE form may run to ~210 bytes before it is rejected)
+            WCTable fct;
+            uint8_t fscratch[64];
+            uint32_t win[kWinWords];
+            uint16_t tanc[256];  // tree depths by pointer jumping: ancestor of internal node 256 + i
+            uint16_t tdep[256];  //                                 distance to it
+            uint32_t rankLast[16];
+            uint32_t vpr[16];     // valPerRank
+            uint32_t wcount[16];  // weight histogram
+            int16_t wnorm[16];
+            uint32_t wcumul[16];
+        };
+    };
+    uint32_t u[8];
+};
+__device__ __forceinline__ uint32_t seg_count(const EncLds& L, int k, int s)
+{
+    return (L.hist2[k >> 1][s] >> (16 * (k & 1))) & 0xFFFFu;
+}
 
 // One instance per encode workgroup (namespace scope, so every access is a DS instruction).
 static __shared__ EncLds sEnc;
@@ -90,11 +112,35 @@ __device__ __forceinline__ uint32_t hash_g(const uint8_t* p, unsigned hlog, unsi
     return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - hlog));
 }
 
+// Number of equal bytes going backwards from a-1 / b-1, at most `lim` (wave-parallel, 64 per step)
+__device__ inline uint32_t wave_back_count(const uint8_t* src, uint32_t a, uint32_t b, uint32_t lim)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t n = 0;
+    while (n < lim) {
+        const uint32_t o = n + lane + 1;
+        const bool diff = (o <= lim) && gb(src + a - o) != gb(src + b - o);
+        const uint64_t m = ballot(diff || o > lim);
+        if (m) return n + (uint32_t)__builtin_ctzll(m);
+        n += 64;
+    }
+    return lim;
+}
+
+// Match search (ZSTD_compressBlock_fast, libzstd 1.4.x) speculated over 64 consecutive visits.
+// The visit positions follow a data-independent recurrence until a match is found, so lane k takes
+// visit k of the round: it hashes its two positions, reads the table (entries (tag << 17) | idx,
+// another tag reads as empty) unless an earlier visit of the round wrote the same slot, and tests
+// the repcode and both candidates; a ballot finds the first hit.  Visits before it commit their
+// table writes (the last writer of a slot wins), the hit is processed as the serial loop does, and
+// the next round starts after it.  Same-slot writers inside a round are found through an LDS filter
+// (one bit per lane per slot), checked exactly only for the lanes whose filter slots collide.
 // Returns nbSeq | lastLiterals << 32.
 __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ src, uint32_t n, unsigned hlog, unsigned mls,
                                                   uint32_t* __restrict__ ht, uint32_t tag, z1::Seq* __restrict__ seqs)
 {
-    const int lane = lane_id();
+    EncLds& L = sEnc;
+    const uint32_t lane = (uint32_t)lane_id();
     src = uni(src);
     n = uni(n);
     hlog = uni(hlog);
@@ -102,87 +148,124 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
     ht = uni(ht);
     tag = uni(tag);
     seqs = uni(seqs);
-    const long iend = (long)n, ilimit = (long)n - 8;
-    long ip0 = 1, anchor = 0;
+    const int32_t iend = (int32_t)n, ilimit = (int32_t)n - 8;
+    int32_t ip0 = 1, anchor = 0;
     uint32_t off1 = 1, off2 = 0;
     uint32_t nbSeq = 0;
+    const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
+    for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
+    lds_sync();
     while (ip0 + 1 < ilimit) {
-        // positions of the next 64 visits (the no-match recurrence)
-        long pk = ip0, q = ip0;
+        // positions of the next 64 visits (the no-match recurrence), scalar
+        int32_t q = ip0;
+        int32_t pk = 0;
         for (int k = 0; k < 64; k++) {
-            if (k == lane) pk = q;
+            pk = ((int)lane == k) ? q : pk;
             q += ((q - anchor) >> 7) + 2;
         }
-        const long pNext = q;
+        const int32_t pNext = q;
         const bool valid = (pk + 1 < ilimit);
         uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu, t0 = 0, t1 = 0;
+        uint64_t M0 = 0, M1 = 0;
         if (valid) {
             h0 = hash_g(src + pk, hlog, mls);
             h1 = hash_g(src + pk + 1, hlog, mls);
             t0 = gld<uint32_t>(ht + h0);
             t1 = gld<uint32_t>(ht + h1);
+            atomicOr((unsigned long long*)&L.filt[h0 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
+            atomicOr((unsigned long long*)&L.filt[h1 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
         }
-        // most recent in-step writer before me, first in-step writer after me
-        uint32_t m0 = 0, m1 = 0;
-        bool has0 = false, has1 = false;
-        int later0 = 64, later1 = 64;
-        for (int j = 0; j < 64; j++) {
-            uint32_t hj0 = readlane_u32(h0, j), hj1 = readlane_u32(h1, j);
-            uint32_t pj = readlane_u32((uint32_t)pk, j);
-            if (j < lane) {
-                if (hj1 == h0) { m0 = pj + 2; has0 = true; } else if (hj0 == h0) { m0 = pj + 1; has0 = true; }
-                if (hj1 == h1) { m1 = pj + 2; has1 = true; } else if (hj0 == h1) { m1 = pj + 1; has1 = true; }
-            } else if (j > lane) {
-                if (later0 == 64 && (hj0 == h0 || hj1 == h0)) later0 = j;
-                if (later1 == 64 && (hj0 == h1 || hj1 == h1)) later1 = j;
-            }
+        L.vh0[lane] = h0;
+        L.vh1[lane] = h1;
+        L.vpk[lane] = (uint32_t)pk;
+        lds_sync();
+        if (valid) {
+            M0 = L.filt[h0 & (kFiltSlots - 1)];
+            M1 = L.filt[h1 & (kFiltSlots - 1)];
         }
-        if (!has0) m0 = ((t0 >> 17) == tag) ? (t0 & 0x1FFFFu) : 0u;
-        if (!has1) m1 = ((t1 >> 17) == tag) ? (t1 & 0x1FFFFu) : 0u;
+        lds_sync();
+        if (valid) {
+            L.filt[h0 & (kFiltSlots - 1)] = 0;
+            L.filt[h1 & (kFiltSlots - 1)] = 0;
+        }
+        // value each slot holds at my visit: the latest earlier writer in this round, else the table
+        uint32_t m0 = ((t0 >> 17) == tag) ? (t0 & 0x1FFFFu) : 0u;
+        uint32_t m1 = ((t1 >> 17) == tag) ? (t1 & 0x1FFFFu) : 0u;
+        for (uint64_t cand = M0 & below; cand;) {
+            const int jj = 63 - __builtin_clzll(cand);
+            const uint32_t pj = L.vpk[jj];
+            if (L.vh1[jj] == h0) { m0 = pj + 2; break; }
+            if (L.vh0[jj] == h0) { m0 = pj + 1; break; }
+            cand &= ~(1ull << jj);
+        }
+        for (uint64_t cand = M1 & below; cand;) {
+            const int jj = 63 - __builtin_clzll(cand);
+            const uint32_t pj = L.vpk[jj];
+            if (L.vh1[jj] == h1) { m1 = pj + 2; break; }
+            if (L.vh0[jj] == h1) { m1 = pj + 1; break; }
+            cand &= ~(1ull << jj);
+        }
         bool rep = false, c0 = false, c1 = false;
         if (valid) {
-            const long ip2 = pk + 2;
-            rep = (off1 > 0) && (ld32u(src + ip2 - off1) == ld32u(src + ip2));
+            const int32_t ip2 = pk + 2;
+            const uint32_t here = ld32u(src + pk + 1);  // bytes pk+1 .. pk+4
+            rep = (off1 > 0) && (ld32u(src + ip2 - (int32_t)off1) == ld32u(src + ip2));
             c0 = (m0 > 1) && (ld32u(src + m0 - 1) == ld32u(src + pk));
-            c1 = (m1 > 1) && (ld32u(src + m1 - 1) == ld32u(src + pk + 1));
+            c1 = (m1 > 1) && (ld32u(src + m1 - 1) == here);
         }
         const uint64_t hits = ballot(rep || c0 || c1);
         const uint64_t vmask = ballot(valid);
         const int f = hits ? __builtin_ctzll(hits) : 64;
         const int lastCommit = hits ? f : (63 - __builtin_clzll(vmask));
-        if (valid && lane <= lastCommit) {
-            const bool w1 = later1 > lastCommit;
-            const bool w0 = (later0 > lastCommit) && (h0 != h1);
+        if (valid && (int)lane <= lastCommit) {
+            // my write survives unless a later committed visit of the round writes the same slot
+            const uint64_t upto = (lastCommit >= 63) ? ~0ull : ((1ull << (lastCommit + 1)) - 1ull);
+            bool w0 = (h0 != h1), w1 = true;
+            for (uint64_t cand = M0 & above & upto; cand && w0;) {
+                const int jj = __builtin_ctzll(cand);
+                if (L.vh0[jj] == h0 || L.vh1[jj] == h0) w0 = false;
+                cand &= cand - 1;
+            }
+            for (uint64_t cand = M1 & above & upto; cand && w1;) {
+                const int jj = __builtin_ctzll(cand);
+                if (L.vh0[jj] == h1 || L.vh1[jj] == h1) w1 = false;
+                cand &= cand - 1;
+            }
             if (w0) gst<uint32_t>(ht + h0, tagged(tag, (uint32_t)pk + 1));
             if (w1) gst<uint32_t>(ht + h1, tagged(tag, (uint32_t)pk + 2));
         }
+        lds_sync();
         if (!hits) {
             wave_sync();
             if (vmask == ~0ull) { ip0 = pNext; continue; }
             break;
         }
         // the match found at visit f, processed exactly as the serial loop does
-        const long ipf = (long)readlane_u32((uint32_t)pk, f);
+        const int32_t ipf = (int32_t)L.vpk[f];
         const bool repf = (ballot(rep) >> f) & 1, c0f = (ballot(c0) >> f) & 1;
         const uint32_t m0f = readlane_u32(m0, f), m1f = readlane_u32(m1, f);
         const uint32_t cur0 = (uint32_t)ipf + 1;
-        long ipm, match0;
+        int32_t ipm, match0;
         uint32_t mLength, offcode;
         if (repf) {
-            const long ip2 = ipf + 2;
-            mLength = (gb(src + (ip2 - 1)) == gb(src + (ip2 - (long)off1 - 1))) ? 1u : 0u;
-            ipm = ip2 - (long)mLength;
-            match0 = ipm - (long)off1;
+            const int32_t ip2 = ipf + 2;
+            mLength = (gb(src + (ip2 - 1)) == gb(src + (ip2 - (int32_t)off1 - 1))) ? 1u : 0u;
+            ipm = ip2 - (int32_t)mLength;
+            match0 = ipm - (int32_t)off1;
             mLength += 4;
             offcode = 0;
         } else {
-            if (c0f) { ipm = ipf; match0 = (long)m0f - 1; }
-            else { ipm = ipf + 1; match0 = (long)m1f - 1; }
+            if (c0f) { ipm = ipf; match0 = (int32_t)m0f - 1; }
+            else { ipm = ipf + 1; match0 = (int32_t)m1f - 1; }
             off2 = off1;
             off1 = (uint32_t)(ipm - match0);
             offcode = off1 + 2;
             mLength = 4;
-            while ((ipm > anchor) && (match0 > 0) && (gb(src + (ipm - 1)) == gb(src + (match0 - 1)))) { ipm--; match0--; mLength++; }
+            const int32_t lim = (ipm - anchor) < match0 ? (ipm - anchor) : match0;
+            const uint32_t back = lim > 0 ? wave_back_count(src, (uint32_t)ipm, (uint32_t)match0, (uint32_t)lim) : 0u;
+            ipm -= (int32_t)back;
+            match0 -= (int32_t)back;
+            mLength += back;
         }
         mLength += wave_match_count(src, (uint32_t)ipm + mLength, (uint32_t)match0 + mLength, (uint32_t)iend);
         if (lane == 0) {
@@ -191,25 +274,27 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
             seqs[nbSeq].mlBase = mLength - 3;
         }
         nbSeq++;
-        ip0 = ipm + (long)mLength;
+        ip0 = ipm + (int32_t)mLength;
         anchor = ip0;
         if (ip0 <= ilimit) {
             if (lane == 0) {
-                ht[hash_g(src + cur0 + 1, hlog, mls)] = tagged(tag, cur0 + 2);
-                ht[hash_g(src + ip0 - 2, hlog, mls)] = tagged(tag, (uint32_t)(ip0 - 2) + 1);
+                gst<uint32_t>(ht + hash_g(src + cur0 + 1, hlog, mls), tagged(tag, cur0 + 2));
+                gst<uint32_t>(ht + hash_g(src + ip0 - 2, hlog, mls), tagged(tag, (uint32_t)(ip0 - 2) + 1));
             }
             if (off2 > 0) {
-                while ((ip0 <= ilimit) && (ld32u(src + ip0) == ld32u(src + ip0 - off2))) {
-                    uint32_t rLength = wave_match_count(src, (uint32_t)ip0 + 4, (uint32_t)ip0 + 4 - off2, (uint32_t)iend) + 4;
-                    uint32_t t = off2; off2 = off1; off1 = t;
+                while ((ip0 <= ilimit) && (ld32u(src + ip0) == ld32u(src + ip0 - (int32_t)off2))) {
+                    const uint32_t rLength = wave_match_count(src, (uint32_t)ip0 + 4, (uint32_t)ip0 + 4 - off2, (uint32_t)iend) + 4;
+                    const uint32_t t = off2;
+                    off2 = off1;
+                    off1 = t;
                     if (lane == 0) {
-                        ht[hash_g(src + ip0, hlog, mls)] = tagged(tag, (uint32_t)ip0 + 1);
+                        gst<uint32_t>(ht + hash_g(src + ip0, hlog, mls), tagged(tag, (uint32_t)ip0 + 1));
                         seqs[nbSeq].litLength = 0;
                         seqs[nbSeq].offset = 1;
                         seqs[nbSeq].mlBase = rLength - 3;
                     }
                     nbSeq++;
-                    ip0 += (long)rLength;
+                    ip0 += (int32_t)rLength;
                     anchor = ip0;
                 }
             }
@@ -532,7 +617,7 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
 }
 
 // FSE_buildCTable_wksp for the weight alphabet (<= 13 symbols, tableLog <= 6), wave-uniform
-__device__ __forceinline__ void fse_build_ctable_small(z1::FseCTable& ct, const int16_t* norm, unsigned maxSymbolValue,
+__device__ __forceinline__ void fse_build_ctable_small(WCTable& ct, const int16_t* norm, unsigned maxSymbolValue,
                                                        unsigned tableLog, uint8_t* tableSymbol, uint32_t* cumul)
 {
     const uint32_t tableSize = 1u << tableLog;
@@ -587,6 +672,19 @@ __device__ __forceinline__ void fse_build_ctable_small(z1::FseCTable& ct, const 
     lds_sync();
 }
 
+__device__ __forceinline__ void wfse_init(uint32_t& st, const WCTable& ct, unsigned symbol)
+{
+    const uint32_t nbBitsOut = (ct.deltaNbBits[symbol] + (1u << 15)) >> 16;
+    const uint32_t v = (nbBitsOut << 16) - ct.deltaNbBits[symbol];
+    st = ct.stateTable[(v >> nbBitsOut) + ct.deltaFindState[symbol]];
+}
+__device__ __forceinline__ void wfse_encode(z1::BitW& bw, uint32_t& st, const WCTable& ct, unsigned symbol)
+{
+    const uint32_t nbBitsOut = (st + ct.deltaNbBits[symbol]) >> 16;
+    z1::bw_add(bw, st, nbBitsOut);
+    st = ct.stateTable[(st >> nbBitsOut) + ct.deltaFindState[symbol]];
+}
+
 // HUF_writeCTable into L.hdr from L.nbBits (wave-uniform; weights and their histogram by ballots).
 // Returns the description size, 0 if it cannot be written (raw weights with > 128 symbols).
 __device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t huffLog)
@@ -634,29 +732,29 @@ __device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t
                     z1::BitW bw;
                     z1::bw_init(bw, op);
                     const uint8_t* ip = L.weights + wtSize;
-                    z1::FseState s1, s2;
+                    uint32_t s1, s2;
                     size_t left = wtSize;
                     if (left & 1) {
-                        z1::fse_init_state2(s1, L.fct, *--ip);
-                        z1::fse_init_state2(s2, L.fct, *--ip);
-                        z1::fse_encode(bw, s1, L.fct, *--ip);
+                        wfse_init(s1, L.fct, *--ip);
+                        wfse_init(s2, L.fct, *--ip);
+                        wfse_encode(bw, s1, L.fct, *--ip);
                     } else {
-                        z1::fse_init_state2(s2, L.fct, *--ip);
-                        z1::fse_init_state2(s1, L.fct, *--ip);
+                        wfse_init(s2, L.fct, *--ip);
+                        wfse_init(s1, L.fct, *--ip);
                     }
                     left -= 2;
                     if (left & 2) {
-                        z1::fse_encode(bw, s2, L.fct, *--ip);
-                        z1::fse_encode(bw, s1, L.fct, *--ip);
+                        wfse_encode(bw, s2, L.fct, *--ip);
+                        wfse_encode(bw, s1, L.fct, *--ip);
                     }
                     while (ip > L.weights) {
-                        z1::fse_encode(bw, s2, L.fct, *--ip);
-                        z1::fse_encode(bw, s1, L.fct, *--ip);
-                        z1::fse_encode(bw, s2, L.fct, *--ip);
-                        z1::fse_encode(bw, s1, L.fct, *--ip);
+                        wfse_encode(bw, s2, L.fct, *--ip);
+                        wfse_encode(bw, s1, L.fct, *--ip);
+                        wfse_encode(bw, s2, L.fct, *--ip);
+                        wfse_encode(bw, s1, L.fct, *--ip);
                     }
-                    z1::fse_flush(bw, s2, L.fct);
-                    z1::fse_flush(bw, s1, L.fct);
+                    z1::bw_add(bw, s2, L.fct.tableLog);
+                    z1::bw_add(bw, s1, L.fct.tableLog);
                     hSize = (uint32_t)(nh + z1::bw_close(bw, op));
                 }
             }
@@ -714,7 +812,7 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     const bool single = n < 256;
     const uint32_t segSize = single ? n : (n + 3) / 4;
     const int nseg = single ? 1 : 4;
-    for (int i = lane; i < 4 * 256; i += 64) (&L.hist4[0][0])[i] = 0;
+    for (int i = lane; i < 2 * 256; i += 64) (&L.hist2[0][0])[i] = 0;
     wave_sync();
     // per-segment histograms
     for (uint32_t i = (uint32_t)lane * 16; i < n; i += 1024) {
@@ -731,7 +829,7 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
         for (int k = 0; k < 16; k++) {
             if (i + k < n) {
                 uint32_t sg = (i + k < boundary) ? sa : sa + 1;
-                atomicAdd(&L.hist4[sg][b[k]], 1u);
+                atomicAdd(&L.hist2[sg >> 1][b[k]], 1u << (16 * (sg & 1)));
             }
         }
     }
@@ -741,7 +839,8 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         int s = lane + 64 * q;
-        c[q] = L.hist4[0][s] + L.hist4[1][s] + L.hist4[2][s] + L.hist4[3][s];
+        const uint32_t h01 = L.hist2[0][s], h23 = L.hist2[1][s];
+        c[q] = (h01 & 0xFFFFu) + (h01 >> 16) + (h23 & 0xFFFFu) + (h23 >> 16);
         L.count[s] = c[q];
         if (c[q]) myMaxSym = (uint32_t)s;
         myLargest = c[q] > myLargest ? c[q] : myLargest;
@@ -800,7 +899,7 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
             uint32_t nbq = ((uint32_t)s <= maxSym) ? L.nbBits[s] : 0;
             L.cw[s] = ((uint32_t)s <= maxSym) ? ((uint32_t)L.val[s] | (nbq << 16)) : 0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) b4[k] += L.hist4[k][s] * nbq;
+            for (int k = 0; k < 4; k++) b4[k] += seg_count(L, k, s) * nbq;
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
