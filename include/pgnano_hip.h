@@ -103,6 +103,10 @@ int pgn_synth_reads_device(pgn_ctx *ctx, size_t nreads, uint64_t seed, uint64_t 
 /* Diagnostics: accumulated shader-clock cycles per kernel phase (out[0..15] encode, out[16..31]
  * decode; all zero unless the context was created with PGN_PHASE_PROFILE=1 in the environment). */
 int pgn_debug_phase_cycles(pgn_ctx *ctx, uint64_t *out, int n);
+/* Diagnostics: per-stream decode records of the first n chunks of the last decode pass
+ * (5 per chunk, 24 bytes each: u64 frame offset, u32 frame bytes, u32 content size,
+ * u32 intermediate offset, i32 decoded bytes or a negative error). */
+int pgn_debug_decode_units(pgn_ctx *ctx, void *out, size_t nchunks);
 
 /* Kernel time (ms, HIP events on the launch stream) of the last batch encode / decode call on ctx. */
 float pgn_ctx_last_encode_ms(pgn_ctx *ctx);

@@ -48,6 +48,7 @@ SIGNATURES = [
      [_VP, _SZ, C.c_uint64, C.c_uint64, C.c_uint64, _VP, _U64P, _U32P, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
       _VP]),
     ("pgn_debug_phase_cycles", C.c_int, [_VP, _VP, C.c_int]),
+    ("pgn_debug_decode_units", C.c_int, [_VP, _VP, C.c_size_t]),
     ("pgn_ctx_last_encode_ms", C.c_float, [_VP]),
     ("pgn_ctx_last_decode_ms", C.c_float, [_VP]),
 ]

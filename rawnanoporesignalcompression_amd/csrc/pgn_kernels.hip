@@ -76,7 +76,7 @@ __host__ __device__ inline EncLayout enc_layout()
 }
 
 struct DecLayout {
-    size_t lit, seqs, tables, bytes;
+    size_t lit, htmp, seqs, tables, bytes;
 };
 __host__ __device__ inline DecLayout dec_layout()
 {
@@ -84,6 +84,7 @@ __host__ __device__ inline DecLayout dec_layout()
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o = align_up(o + n + 64, 256); return r; };
     l.lit = take(kMaxStream);
+    l.htmp = take((size_t)64 * kSliceCap);
     l.seqs = take(12 * (size_t)kMaxDecSeq);
     l.tables = take(3 * sizeof(z1::FseDTable));
     l.bytes = o;
@@ -314,6 +315,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
     DecScratch S;
     S.lit = sbase + lay.lit;
+    S.htmp = sbase + lay.htmp;
     S.seqs = (uint32_t*)(sbase + lay.seqs);
     S.maxSeq = kMaxDecSeq;
     S.tables = (z1::FseDTable*)(sbase + lay.tables);
@@ -458,6 +460,7 @@ struct pgn_ctx {
     size_t decSlots = 0;
     uint8_t* decChunks = nullptr;  // G * kChunkInterBytes + units
     size_t decG = 0;
+    DecUnit* lastUnits = nullptr;  // decode records of the last pass (diagnostics)
     uint32_t* queues = nullptr;    // one work counter per sub-batch pass
     size_t nQueues = 0;
     // host-call staging (device buffers)
@@ -701,6 +704,7 @@ static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const 
     a.status = d_status;
     a.inter = c->decChunks;
     a.units = (DecUnit*)(c->decChunks + G * kChunkInterBytes);
+    c->lastUnits = a.units;
     a.slotScratch = c->decScratch;
     a.slotBytes = dec_layout().bytes;
     a.prof = c->prof ? c->prof + kPhases : nullptr;
@@ -754,6 +758,18 @@ int pgn_debug_phase_cycles(pgn_ctx* c, uint64_t* out, int n)
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, c->prof, sizeof(uint64_t) * 2 * kPhases, hipMemcpyDeviceToHost));
+    return PGN_OK;
+}
+
+// Diagnostics: the per-stream decode records {frame offset, length, content size, offset, result}
+// of the first n chunks of the last decode pass (24 bytes each, 5 per chunk).
+int pgn_debug_decode_units(pgn_ctx* c, void* out, size_t nchunks)
+{
+    if (!c || !out) return PGN_ERR_INVALID_ARG;
+    if (!c->lastUnits || nchunks > c->decG) return PGN_ERR_INVALID_ARG;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, c->lastUnits, nchunks * kStreams * sizeof(DecUnit), hipMemcpyDeviceToHost));
     return PGN_OK;
 }
 

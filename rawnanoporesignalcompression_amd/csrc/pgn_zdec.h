@@ -1,25 +1,34 @@
 // pgn_zdec.h -- one wave decodes the zstd frame(s) of one stream (ZSTD_decompress semantics, the
-// call at C5.hpp:588-667).  Headers, Huffman/FSE table builds and the sequence list run on lane 0
-// with the shared zstd1_dec.h code; raw/RLE blocks, literal copies and match copies use the whole
-// wave; the (up to four) Huffman streams of a literals section are decoded one per lane.
+// call at C5.hpp:588-667).  Frame/block headers and the sequence list are parsed wave-uniformly;
+// the Huffman table description is staged into LDS and parsed there; raw/RLE blocks, literal and
+// match copies use the whole wave; the four Huffman streams of a literals section are decoded by
+// all 64 lanes (16 per stream, speculative start + synchronisation, see huf_decode4_wave).
 #pragma once
 #include "pgn_wave.h"
 #include "zstd1_dec.h"
 
 namespace pgn {
 
-constexpr int kRec = 16;          // boundary positions recorded per lane for the synchronisation check
-constexpr int kStgBytes = 144;    // per-lane LDS staging of compressed bits per round (128 + lookahead)
-constexpr int32_t kRoundBits = 1024;
+constexpr int kBmpBits = 256;            // speculative boundaries recorded per lane: bit d = position S - d
+constexpr int32_t kRoundBits = 512;      // phase-1 bits per round
+constexpr int kStgWords = 20;            // staged bytes per lane per round: 80 >= (512 + 16 + 31) / 8 + 8
+constexpr uint32_t kSliceCap = 8192;     // speculative symbols kept per lane (htmp slice)
+constexpr int kBnd = 24;                 // stream bytes [S/8 - 20, S/8 + 4) cached per lane for the walk
+constexpr int kBndBelow = 20;
 
 struct DecLds {
     uint16_t tab[1 << z1::kHufTableLogMax];  // Huffman decode table: symbol | nbBits << 8
-    uint32_t stg[64][kStgBytes / 4];         // per-lane staged stream bytes of the current round
-    uint32_t rec[64][kRec];                  // speculative decode: first boundaries per lane
-    uint32_t cnt[64], startp[64], endp[64], exitp[64], tstart[64], tcount[64];
+    uint32_t bmp[64][kBmpBits / 32];         // speculative decode: boundary bitmap below each lane start
+    uint32_t stg[64][kStgWords];             // staged stream bytes of the current round, per lane
+    uint8_t bnd[64][kBnd];                   // bytes around each lane's start (phase-2 walk)
+    uint32_t cnt[64], startp[64], endp[64], exitp[64], skip[64], extra[64], obase[64], syncd[64];
     uint8_t wts[256];                        // weights of the current table
     uint8_t order[256];                      // symbols sorted by (weight, symbol)
-    z1::FseDTable fscr;                      // weights FSE table scratch
+    uint8_t hbuf[272];                       // staged Huffman table description (zero padded)
+    z1::FseDEntry wdt[64];                   // weights FSE decode table (tableLog <= 6)
+    int16_t wnorm[16];
+    uint16_t wnext[16];
+    uint32_t wrank[16];
     uint32_t u[16];
 };
 
@@ -28,6 +37,7 @@ static __shared__ DecLds sDec;
 
 struct DecScratch {
     uint8_t* lit;           // literals of a block with sequences (<= 128 KiB)
+    uint8_t* htmp;          // 64 * kSliceCap speculative Huffman symbols
     uint32_t* seqs;         // decoded sequences: {litLength, matchLength, offset} triples
     uint32_t maxSeq;
     z1::FseDTable* tables;  // ll, of, ml
@@ -71,84 +81,278 @@ __device__ __forceinline__ uint32_t rb_huf(RevBits& r, int32_t& pos, unsigned tl
 }
 
 // ---------------------------------------------------------------------------------------------
-// Round-staged reader: lane l's stream bytes [base, base + kStgBytes) live in sDec.stg[l]; stage
-// positions are bit offsets from base*8.  W caches 64 bits at stage word index wi.
+// Backward reader over a global stream for one lane: W holds bits [wlo, wlo + 64) (wlo a multiple of
+// 32), nx the 32 bits below it, loaded one refill ahead.  Bits outside [0, 8*sl) read as zero.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void stage_round(const uint8_t* __restrict__ src, int32_t roundHi, int lane, int32_t& base)
+__device__ __forceinline__ uint32_t ld_word(const uint8_t* s, int32_t sl, int32_t bytePos)
 {
-    const int32_t byteHi = (roundHi + 7) >> 3;
-    base = byteHi - kStgBytes;
-    uint32_t* d = sDec.stg[lane];
-    if (base >= 0) {
-        uint4 v[kStgBytes / 16];
+    if (bytePos >= 0 && bytePos + 4 <= sl) return ld32u(s + bytePos);
+    uint32_t v = 0;
 #pragma unroll
-        for (int q = 0; q < kStgBytes / 16; q++) v[q] = gld<uint4>(src + base + 16 * q);
+    for (int b = 0; b < 4; b++) {
+        const int32_t i = bytePos + b;
+        if (i >= 0 && i < sl) v |= (uint32_t)gb(s + i) << (8 * b);
+    }
+    return v;
+}
+struct GBits {
+    uint64_t W;
+    int32_t wlo;
+    uint32_t nx;
+};
+__device__ __forceinline__ void gbits_init(GBits& g, const uint8_t* s, int32_t sl, int32_t q)
+{
+    g.wlo = ((q >> 5) - 1) * 32;
+    const int32_t b = g.wlo >> 3;
+    g.W = (uint64_t)ld_word(s, sl, b) | ((uint64_t)ld_word(s, sl, b + 4) << 32);
+    g.nx = ld_word(s, sl, b - 4);
+}
+// the tl bits just below q (q decreases by at most tl between calls)
+__device__ __forceinline__ uint32_t gbits_peek(GBits& g, const uint8_t* s, int32_t sl, int32_t q, unsigned tl)
+{
+    if (q - (int32_t)tl < g.wlo) {
+        g.W = (g.W << 32) | g.nx;
+        g.wlo -= 32;
+        g.nx = ld_word(s, sl, (g.wlo >> 3) - 4);
+    }
+    return (uint32_t)(g.W >> (q - (int32_t)tl - g.wlo)) & ((1u << tl) - 1u);
+}
+
+// Round staging: round r of a lane covers q in (hi - 512, hi] and stages bytes [base, base + 80)
+// with base = 4 * floor((hi - 528) / 32), so bits [q - tl, q) are always inside.
+__device__ __forceinline__ int32_t round_base(int32_t hi) { return ((hi - kRoundBits - 16) >> 5) * 4; }
+__device__ __forceinline__ void round_load(uint4 v[5], const uint8_t* s, int32_t sl, int32_t base)
+{
+    if (base >= 0 && base + 4 * kStgWords <= sl) {
 #pragma unroll
-        for (int q = 0; q < kStgBytes / 16; q++) {
-            d[4 * q] = v[q].x; d[4 * q + 1] = v[q].y; d[4 * q + 2] = v[q].z; d[4 * q + 3] = v[q].w;
-        }
-    } else {  // the first bytes of the stream: zero below byte 0
-        for (int q = 0; q < kStgBytes / 4; q++) {
-            uint32_t v = 0;
+        for (int i = 0; i < 5; i++) v[i] = gld<uint4>(s + base + 16 * i);
+    } else {
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const int32_t idx = base + 4 * q + b;
-                if (idx >= 0 && idx < byteHi) v |= (uint32_t)gb(src + idx) << (8 * b);
-            }
-            d[q] = v;
-        }
+        for (int i = 0; i < 5; i++)
+            v[i] = make_uint4(ld_word(s, sl, base + 16 * i), ld_word(s, sl, base + 16 * i + 4),
+                              ld_word(s, sl, base + 16 * i + 8), ld_word(s, sl, base + 16 * i + 12));
     }
 }
-struct StgBits {
-    uint64_t W;   // stage bits [32*wi, 32*wi + 64)
-    int32_t wi;   // word index of W's low word
-};
-__device__ __forceinline__ void sb_fill(StgBits& r, int lane, int32_t q)  // q: stage bit position
+// the tl bits below local bit position x (x - tl >= 0) of the lane's staged bytes
+__device__ __forceinline__ uint32_t stg_peek(int lane, int32_t x, unsigned tl)
 {
-    int32_t wi = (q >> 5) - 1;
-    wi = wi < 0 ? 0 : wi;
-    r.wi = wi;
-    r.W = (uint64_t)sDec.stg[lane][wi] | ((uint64_t)sDec.stg[lane][wi + 1] << 32);
-}
-// decode one symbol whose code ends at stage bit q (bits [q - tl, q)); returns the table entry
-__device__ __forceinline__ uint32_t sb_huf(StgBits& r, int lane, int32_t q, unsigned tl)
-{
-    if (q - (int32_t)tl < 32 * r.wi || q > 32 * r.wi + 64) sb_fill(r, lane, q);
-    const int32_t lo = q - (int32_t)tl;
-    const uint32_t idx = (lo >= 32 * r.wi) ? (uint32_t)(r.W >> (lo - 32 * r.wi)) : (uint32_t)(r.W << (32 * r.wi - lo));
-    return sDec.tab[idx & ((1u << tl) - 1)];
+    const int32_t lo = x - (int32_t)tl;
+    const int32_t w = lo >> 5;
+    const uint64_t v = (uint64_t)sDec.stg[lane][w] | ((uint64_t)sDec.stg[lane][w + 1] << 32);
+    return (uint32_t)(v >> (lo & 31)) & ((1u << tl) - 1u);
 }
 
 // ---------------------------------------------------------------------------------------------
-// Huffman table description -> decode table in LDS (HUF_readStats + HUF_readDTableX1).  The weight
-// list is parsed on lane 0; ranking and the table fill use the whole wave.  Returns header bytes
-// consumed (0 = corrupt); *tlOut = table log.
+// Huffman table description (HUF_readStats + HUF_readDTableX1), wave-uniform over an LDS copy.
 // ---------------------------------------------------------------------------------------------
+// FSE_readNCount over LDS bytes already zero-padded to hb >= 8 (zstd1_dec.h fse_read_ncount).
+__device__ __forceinline__ size_t ncount_lds(int16_t* norm, unsigned* maxSVPtr, unsigned* tableLogPtr, const uint8_t* istart,
+                                             size_t srcSize, size_t hb, unsigned maxLogAllowed)
+{
+    const uint8_t* ip = istart;
+    const uint8_t* iend = istart + hb;
+    unsigned maxSV1 = *maxSVPtr + 1;
+    int previous0 = 0;
+    for (unsigned i = 0; i < maxSV1; i++) norm[i] = 0;
+    uint32_t bitStream = z1::rd32(ip);
+    unsigned nbBits = (bitStream & 0xF) + z1::kFseMinTableLog;
+    if (nbBits > maxLogAllowed) return 0;
+    bitStream >>= 4;
+    int bitCount = 4;
+    *tableLogPtr = nbBits;
+    int remaining = (1 << nbBits) + 1;
+    int threshold = 1 << nbBits;
+    nbBits++;
+    unsigned charnum = 0;
+    while ((remaining > 1) & (charnum <= *maxSVPtr)) {
+        if (previous0) {
+            unsigned n0 = charnum;
+            while ((bitStream & 0xFFFF) == 0xFFFF) {
+                n0 += 24;
+                if (ip < iend - 5) {
+                    ip += 2;
+                    bitStream = z1::rd32(ip) >> bitCount;
+                } else {
+                    bitStream >>= 16;
+                    bitCount += 16;
+                }
+            }
+            while ((bitStream & 3) == 3) {
+                n0 += 3;
+                bitStream >>= 2;
+                bitCount += 2;
+            }
+            n0 += bitStream & 3;
+            bitCount += 2;
+            if (n0 > *maxSVPtr) return 0;
+            while (charnum < n0) norm[charnum++] = 0;
+            if ((ip <= iend - 7) || (ip + (bitCount >> 3) <= iend - 4)) {
+                ip += bitCount >> 3;
+                bitCount &= 7;
+                bitStream = z1::rd32(ip) >> bitCount;
+            } else {
+                bitStream >>= 2;
+            }
+        }
+        {
+            int const max = (2 * threshold - 1) - remaining;
+            int count;
+            if ((int)(bitStream & (uint32_t)(threshold - 1)) < max) {
+                count = (int)(bitStream & (uint32_t)(threshold - 1));
+                bitCount += (int)nbBits - 1;
+            } else {
+                count = (int)(bitStream & (uint32_t)(2 * threshold - 1));
+                if (count >= threshold) count -= max;
+                bitCount += (int)nbBits;
+            }
+            count--;
+            remaining -= count < 0 ? -count : count;
+            norm[charnum++] = (int16_t)count;
+            previous0 = !count;
+            while (remaining < threshold) {
+                nbBits--;
+                threshold >>= 1;
+            }
+            if ((ip <= iend - 7) || (ip + (bitCount >> 3) <= iend - 4)) {
+                ip += bitCount >> 3;
+                bitCount &= 7;
+            } else {
+                bitCount -= (int)(8 * (iend - 4 - ip));
+                ip = iend - 4;
+            }
+            bitStream = z1::rd32(ip) >> (bitCount & 31);
+        }
+    }
+    if (remaining != 1) return 0;
+    if (bitCount > 32) return 0;
+    *maxSVPtr = charnum - 1;
+    ip += (bitCount + 7) >> 3;
+    const size_t used = (size_t)(ip - istart);
+    if (used > srcSize) return 0;
+    return used;
+}
+
+// FSE_buildDTable for the weight alphabet (tableLog <= 6) into sDec.wdt
+__device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxSV, unsigned tableLog)
+{
+    const uint32_t tableSize = 1u << tableLog;
+    const uint32_t mask = tableSize - 1;
+    const uint32_t step = (tableSize >> 1) + (tableSize >> 3) + 3;
+    uint32_t highThreshold = tableSize - 1;
+    for (unsigned sy = 0; sy <= maxSV; sy++) {
+        if (norm[sy] == -1) {
+            sDec.wdt[highThreshold--].symbol = (uint8_t)sy;
+            sDec.wnext[sy] = 1;
+        } else {
+            sDec.wnext[sy] = (uint16_t)norm[sy];
+        }
+    }
+    uint32_t position = 0;
+    for (unsigned sy = 0; sy <= maxSV; sy++) {
+        for (int i = 0; i < norm[sy]; i++) {
+            sDec.wdt[position].symbol = (uint8_t)sy;
+            position = (position + step) & mask;
+            while (position > highThreshold) position = (position + step) & mask;
+        }
+    }
+    if (position != 0) return false;
+    lds_sync();
+    for (uint32_t u = 0; u < tableSize; u++) {
+        const uint8_t sy = sDec.wdt[u].symbol;
+        const uint32_t nextState = sDec.wnext[sy];
+        sDec.wnext[sy] = (uint16_t)(nextState + 1);
+        const uint8_t nb = (uint8_t)(tableLog - z1::highbit32(nextState));
+        sDec.wdt[u].nbBits = nb;
+        sDec.wdt[u].newState = (uint16_t)((nextState << nb) - tableSize);
+    }
+    lds_sync();
+    return true;
+}
+
+// Returns header bytes consumed (0 = corrupt); *tlOut = table log.  Fills sDec.tab.
 __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut)
 {
     const int lane = lane_id();
     src = uni(src);
     srcSize = uni((uint64_t)srcSize);
-    if (lane == 0) {
-        unsigned nbW = 0;
-        size_t used = z1::huf_read_weights(sDec.wts, &nbW, src, srcSize, sDec.fscr);
-        unsigned tl = used ? z1::huf_complete_weights(sDec.wts, nbW) : 0;
-        sDec.u[8] = (uint32_t)used;
-        sDec.u[9] = tl;
-        sDec.u[10] = nbW + 1;
+    if (srcSize < 1) return 0;
+    // stage the description (at most 129 bytes are part of it)
+    const uint32_t nst = srcSize < 256 ? (uint32_t)srcSize : 256u;
+    for (uint32_t i = (uint32_t)lane; i < 272; i += 64) sDec.hbuf[i] = i < nst ? gb(src + i) : (uint8_t)0;
+    lds_sync();
+    const uint32_t iSize = sDec.hbuf[0];
+    uint32_t nbW = 0;
+    size_t used = 0;
+    if (iSize >= 128) {
+        nbW = iSize - 127;
+        const uint32_t bytes = (nbW + 1) / 2;
+        if (bytes + 1 > srcSize) return 0;
+        for (uint32_t nn = 2u * (uint32_t)lane; nn < nbW; nn += 128) {
+            const uint8_t v = sDec.hbuf[1 + nn / 2];
+            sDec.wts[nn] = v >> 4;
+            if (nn + 1 < nbW) sDec.wts[nn + 1] = v & 15;
+        }
+        used = bytes + 1;
+    } else {
+        if (iSize + 1 > srcSize) return 0;
+        // FSE_readNCount pads a short header with zeros to 8 bytes
+        if (iSize < 8 && (uint32_t)lane < 8 && (uint32_t)lane >= iSize) sDec.hbuf[1 + lane] = 0;
+        lds_sync();
+        unsigned maxSV = z1::kHufTableLogMax, tl = 0;
+        const size_t nc = ncount_lds(sDec.wnorm, &maxSV, &tl, sDec.hbuf + 1, iSize, iSize < 8 ? 8 : iSize, 6);
+        if (nc == 0 || nc >= iSize) return 0;
+        lds_sync();
+        if (!wdtable_build(sDec.wnorm, maxSV, tl)) return 0;
+        z1::BitR br;
+        if (!z1::br_init(br, sDec.hbuf + 1 + nc, iSize - nc)) return 0;
+        uint32_t st1 = z1::br_read(br, tl), st2 = z1::br_read(br, tl);
+        // alternate states; stop when the stream overruns (FSE_decompress_usingDTable tail rule)
+        while (true) {
+            if (nbW > 253) return 0;
+            const z1::FseDEntry e1 = sDec.wdt[st1];
+            sDec.wts[nbW++] = e1.symbol;
+            st1 = e1.newState + z1::br_read(br, e1.nbBits);
+            if (br.pos < 0) { sDec.wts[nbW++] = sDec.wdt[st2].symbol; break; }
+            if (nbW > 253) return 0;
+            const z1::FseDEntry e2 = sDec.wdt[st2];
+            sDec.wts[nbW++] = e2.symbol;
+            st2 = e2.newState + z1::br_read(br, e2.nbBits);
+            if (br.pos < 0) { sDec.wts[nbW++] = sDec.wdt[st1].symbol; break; }
+        }
+        used = iSize + 1;
     }
     lds_sync();
-    const size_t used = sDec.u[8];
-    const unsigned tl = sDec.u[9];
-    const unsigned nbSym = sDec.u[10];
-    if (used == 0 || tl == 0) return 0;
-    // per-weight counts and exclusive ranks of my four symbols (weights 1..12, 10 bits each)
+    // HUF_readStats tail: implied last weight and table log (weights > 12 are corrupt)
     uint32_t w4[4];
+    uint32_t wsum = 0, bad = 0, r1 = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t sym = 4u * (uint32_t)lane + (uint32_t)q;
-        w4[q] = (sym < nbSym) ? sDec.wts[sym] : 0u;
+        w4[q] = (sym < nbW) ? sDec.wts[sym] : 0u;
+        bad |= w4[q] > z1::kHufTableLogMax;
+        wsum += w4[q] > z1::kHufTableLogMax ? 0u : ((1u << w4[q]) >> 1);
+        r1 += w4[q] == 1;
     }
+    if (ballot(bad != 0)) return 0;
+    const uint32_t weightTotal = wave_sum(wsum);
+    if (weightTotal == 0) return 0;
+    const unsigned tl = z1::highbit32(weightTotal) + 1;
+    if (tl > z1::kHufTableLogMax) return 0;
+    const uint32_t rest = (1u << tl) - weightTotal;
+    if ((1u << z1::highbit32(rest)) != rest) return 0;
+    const unsigned lastWeight = z1::highbit32(rest) + 1;
+    const uint32_t rank1 = wave_sum(r1) + (lastWeight == 1);
+    if ((rank1 < 2) || (rank1 & 1)) return 0;
+    const unsigned nbSym = nbW + 1;
+    {   // the last symbol takes the implied weight
+        const uint32_t q = nbW & 3u;
+        if ((uint32_t)lane == (nbW >> 2)) {
+#pragma unroll
+            for (int qq = 0; qq < 4; qq++) if ((uint32_t)qq == q) w4[qq] = lastWeight;
+        }
+        if (lane == 0) sDec.wts[nbW] = (uint8_t)lastWeight;
+    }
+    // per-weight counts and exclusive ranks of my four symbols (weights 1..12, 10 bits each)
     uint32_t rankIdx[4] = {0, 0, 0, 0};
     uint32_t cntW[13];
     uint32_t before[13];  // symbols of smaller weight, in order[] terms
@@ -191,7 +395,7 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t sym = 4u * (uint32_t)lane + (uint32_t)q;
-        if (w4[q]) sDec.order[before[w4[q]] + rankIdx[q]] = (uint8_t)sym;
+        if (sym < nbSym && w4[q]) sDec.order[before[w4[q]] + rankIdx[q]] = (uint8_t)sym;
     }
     lds_sync();
     const uint32_t tsize = 1u << tl;
@@ -210,14 +414,41 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
 
 // ---------------------------------------------------------------------------------------------
 // Four Huffman streams decoded by the whole wave: 16 lanes per stream.  Each lane decodes a bit
-// range of its stream starting at an assumed codeword boundary (phase 1) and records its first
-// boundaries; one lane per stream then chains the true starts: a lane whose recorded boundaries
-// contain the previous lane's exit has self-synchronised, otherwise that range is re-decoded serially
-// (phase 2); finally every lane decodes its exact symbols from its true start into place (phase 3).
-// Compressed bits are staged per lane in LDS, one 1024-bit round at a time, so the inner loops only
-// touch LDS and the output stores never stall them.  Returns false on a malformed stream.
+// range of its stream from an assumed codeword boundary (phase 1), keeping the symbols in its
+// scratch slice and its first boundaries in LDS.  One lane per stream then walks the true path
+// across the 15 lane borders (phase 2): where it meets a boundary the neighbour recorded, the
+// neighbour's speculative symbols from there on are the true ones; the few symbols before that
+// point are written by the walker.  Finally every lane copies its synchronised symbols into place
+// (phase 3).  Returns false on a malformed stream.
 // ---------------------------------------------------------------------------------------------
-__device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs)
+// the walker's bit peek: from the lane's cached border bytes when they cover [q - tl, q)
+__device__ __forceinline__ uint32_t walk_peek(int l, int32_t Sl, const uint8_t* s, int32_t sl, int32_t q, unsigned tl)
+{
+    const int32_t lo = q - (int32_t)tl;
+    const uint32_t mask = (1u << tl) - 1u;
+    if (lo < 0) {  // bits below the stream start read as zero
+        uint32_t v = 0;
+        for (int k = 0; k < 2; k++)
+            if (k < sl) v |= (uint32_t)gb(s + k) << (8 * k);
+        v &= (1u << q) - 1u;
+        return (v << (-lo)) & mask;
+    }
+    const int32_t b0 = (Sl >> 3) - kBndBelow;
+    const int32_t i0 = (lo >> 3) - b0;
+    uint32_t v;
+    if (i0 >= 0 && i0 + 2 < kBnd) {
+        v = (uint32_t)sDec.bnd[l][i0] | ((uint32_t)sDec.bnd[l][i0 + 1] << 8) | ((uint32_t)sDec.bnd[l][i0 + 2] << 16);
+    } else {
+        const int32_t b = lo >> 3;
+        v = 0;
+        for (int k = 0; k < 3; k++)
+            if (b + k < sl) v |= (uint32_t)gb(s + b + k) << (8 * k);
+    }
+    return (v >> (lo & 7)) & mask;
+}
+
+__device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
+                                              uint8_t* htmp)
 {
     const int lane = lane_id();
     tl = uni(tl);
@@ -225,6 +456,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     remain = uni((uint64_t)remain);
     dst = uni(dst);
     rs = uni(rs);
+    htmp = uni(htmp);
     const int k = lane >> 4, j = lane & 15;
     if (remain < 6) return false;
     const size_t l1 = gld<uint16_t>(hp), l2 = gld<uint16_t>(hp + 2), l3 = gld<uint16_t>(hp + 4);
@@ -233,124 +465,143 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     const uint32_t seg = (rs + 3) / 4;
     if (seg * 3 > rs) return false;
     const size_t so = (k == 0) ? 0 : (k == 1 ? l1 : (k == 2 ? l1 + l2 : l1 + l2 + l3));
-    const size_t sl = (k == 0) ? l1 : (k == 1 ? l2 : (k == 2 ? l3 : l4));
+    const int32_t sl = (int32_t)((k == 0) ? l1 : (k == 1 ? l2 : (k == 2 ? l3 : l4)));
     const uint32_t nsym = (k == 3) ? rs - 3 * seg : seg;
     const uint8_t* src = hp + 6 + so;
     const uint8_t lastB = sl > 0 ? gb(src + sl - 1) : 0;
     if (ballot(lastB == 0)) return false;
-    const int32_t B = (int32_t)(sl - 1) * 8 + (int32_t)z1::highbit32(lastB);
+    const int32_t B = (sl - 1) * 8 + (int32_t)z1::highbit32(lastB);
     const int32_t Lr = (B + 15) >> 4;
     const int32_t S = (B > j * Lr) ? B - j * Lr : 0;
     const int32_t E = (B > (j + 1) * Lr) ? B - (j + 1) * Lr : 0;
-
-    // ---- phase 1: speculative decode of (E, S], counting symbols, recording the first boundaries
-    int32_t pos = S;
-    uint32_t c = 0;
+    // border bytes for the walk
+    {
+        const int32_t b0 = (S >> 3) - kBndBelow;
+#pragma unroll
+        for (int w = 0; w < kBnd / 4; w++) {
+            const uint32_t v = ld_word(src, sl, b0 + 4 * w);
+            *(uint32_t*)&sDec.bnd[lane][4 * w] = v;
+        }
+    }
+    // ---- phase 1: speculative decode of (E, S] into the lane's slice
+#pragma unroll
+    for (int w = 0; w < kBmpBits / 32; w++) sDec.bmp[lane][w] = 0;
+    uint8_t* slice = htmp + (size_t)lane * kSliceCap;
+    int32_t q = S;
+    uint32_t c = 0, acc = 0;
     {
         const int32_t rounds = (int32_t)wave_max((uint32_t)((S - E + kRoundBits - 1) / kRoundBits));
+        uint4 nx[5];
+        round_load(nx, src, sl, round_base(S));
         for (int32_t r = 0; r < rounds; r++) {
             const int32_t hi = S - r * kRoundBits;
-            const int32_t lo = (hi - kRoundBits > E) ? hi - kRoundBits : E;
-            int32_t base = 0;
-            if (hi > E) stage_round(src, pos, lane, base);
+            const int32_t base = round_base(hi);
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                sDec.stg[lane][4 * i] = nx[i].x;
+                sDec.stg[lane][4 * i + 1] = nx[i].y;
+                sDec.stg[lane][4 * i + 2] = nx[i].z;
+                sDec.stg[lane][4 * i + 3] = nx[i].w;
+            }
+            if (r + 1 < rounds) round_load(nx, src, sl, round_base(hi - kRoundBits));  // next round, in flight
             lds_sync();
-            if (hi > E) {
-                StgBits sb;
-                sb_fill(sb, lane, pos - 8 * base);
-                while (pos > lo) {
-                    if (c < (uint32_t)kRec) sDec.rec[lane][c] = (uint32_t)pos;
-                    const uint32_t e = sb_huf(sb, lane, pos - 8 * base, tl);
-                    pos -= (int32_t)(e >> 8);
-                    c++;
+            const int32_t lo = (hi - kRoundBits > E) ? hi - kRoundBits : E;
+            const int32_t b8 = 8 * base;
+            while (q > lo) {
+                const int32_t d = S - q;
+                if (d < kBmpBits) atomicOr(&sDec.bmp[lane][d >> 5], 1u << (d & 31));
+                const uint32_t e = sDec.tab[stg_peek(lane, q - b8, tl)];
+                q -= (int32_t)(e >> 8);
+                acc |= (e & 0xFFu) << (8 * (c & 3));
+                c++;
+                if ((c & 3) == 0) {
+                    if (c <= kSliceCap) gst<uint32_t>(slice + c - 4, acc);
+                    acc = 0;
                 }
             }
             lds_sync();
         }
+        if ((c & 3) && c <= kSliceCap)
+            for (uint32_t t = c & ~3u; t < c; t++) gst<uint8_t>(slice + t, (uint8_t)(acc >> (8 * (t & 3))));
     }
     sDec.cnt[lane] = c;
     sDec.startp[lane] = (uint32_t)S;
     sDec.endp[lane] = (uint32_t)E;
-    sDec.exitp[lane] = (uint32_t)pos;
+    sDec.exitp[lane] = (uint32_t)q;
     lds_sync();
-    // ---- phase 2: chain the true starts (one lane per stream)
+    // ---- phase 2: walk the true path across the borders (one lane per stream)
+    uint8_t* sdst = dst + (size_t)seg * (size_t)k;
     if (j == 0) {
-        sDec.tstart[lane] = (uint32_t)S;
-        sDec.tcount[lane] = c;
-        int32_t T = pos;
-        RevBits r2;
-        r2.s = src;
+        sDec.skip[lane] = 0;
+        sDec.syncd[lane] = 0;
+        sDec.extra[lane] = 0;
+        sDec.obase[lane] = 0;
+        uint32_t out = c;  // symbols placed so far in this stream
+        int32_t T = q;
         for (int jj = 1; jj < 16; jj++) {
             const int l = lane + jj;
             const uint32_t cl = sDec.cnt[l];
-            const uint32_t m = cl < (uint32_t)kRec ? cl : (uint32_t)kRec;
-            const int32_t El = (int32_t)sDec.endp[l];
-            sDec.tstart[l] = (uint32_t)T;
-            // walk the true path from T until it meets a boundary the speculative decode recorded
+            const int32_t Sl = (int32_t)sDec.startp[l], El = (int32_t)sDec.endp[l];
+            sDec.obase[l] = out;
             int32_t p = T;
-            uint32_t extra = 0, idx = 0;
+            uint32_t ex = 0;
             bool synced = false;
-            rb_fill(r2, p);
             while (p > El) {
-                while (idx < m && (int32_t)sDec.rec[l][idx] > p) idx++;
-                if (idx < m && (int32_t)sDec.rec[l][idx] == p) { synced = true; break; }
-                if (idx >= m) break;  // past the recorded boundaries: finish serially below
-                rb_huf(r2, p, tl);
-                extra++;
+                const int32_t d = Sl - p;
+                if (d >= kBmpBits) break;  // past the recorded boundaries: finish serially below
+                if ((sDec.bmp[l][d >> 5] >> (d & 31)) & 1u) { synced = true; break; }
+                const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, p, tl)];
+                p -= (int32_t)(e >> 8);
+                if (out + ex < nsym) gst<uint8_t>(sdst + out + ex, (uint8_t)e);
+                ex++;
             }
             if (synced) {
-                sDec.tcount[l] = extra + (cl - idx);
+                // speculative symbols before the meeting point: boundaries recorded above it
+                const int32_t d = Sl - p;
+                uint32_t idx = 0;
+                for (int w = 0; w < (d >> 5); w++) idx += (uint32_t)__builtin_popcount(sDec.bmp[l][w]);
+                if (d & 31) idx += (uint32_t)__builtin_popcount(sDec.bmp[l][d >> 5] & ((1u << (d & 31)) - 1u));
+                sDec.skip[l] = idx;
+                sDec.syncd[l] = (uint32_t)d;
                 T = (int32_t)sDec.exitp[l];
-            } else {
-                while (p > El) { rb_huf(r2, p, tl); extra++; }
-                sDec.tcount[l] = extra;
+                out += ex + (cl - idx);
+            } else {  // no common boundary: the walker decodes the rest of the range itself
+                while (p > El) {
+                    const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, p, tl)];
+                    p -= (int32_t)(e >> 8);
+                    if (out + ex < nsym) gst<uint8_t>(sdst + out + ex, (uint8_t)e);
+                    ex++;
+                }
+                sDec.skip[l] = cl;
                 T = p;
+                out += ex;
             }
+            sDec.extra[l] = ex;
         }
-        sDec.u[12 + k] = (uint32_t)T;  // true end of the stream (must be 0)
+        sDec.u[12 + k] = (uint32_t)T;    // true end of the stream (must be 0)
+        sDec.u[8 + k] = out;             // symbols of the stream
     }
     lds_sync();
-    // ---- phase 3: exact decode into place
-    const uint32_t tc = sDec.tcount[lane];
-    const uint32_t incl = wave_incl_sum(tc);
-    // per-lane source lanes: __shfl (ds_bpermute), not readlane (which needs a uniform index)
-    const uint32_t grpEnd = (uint32_t)__shfl((int)incl, 16 * k + 15, 64);
-    const uint32_t grpBase = (uint32_t)__shfl((int)incl, (16 * k + 63) & 63, 64);
-    const uint32_t grpStart = (k == 0) ? 0u : grpBase;
-    const bool good = (grpEnd - grpStart == nsym) && ((int32_t)sDec.u[12 + k] == 0);
+    const bool good = (sDec.u[8 + k] == nsym) && ((int32_t)sDec.u[12 + k] == 0);
     if (ballot(!good)) return false;
-    uint8_t* out = dst + (size_t)seg * (size_t)k + (incl - tc - grpStart);
-    const int32_t T0 = (int32_t)sDec.tstart[lane];
-    pos = T0;
-    uint32_t i = 0, acc = 0;
-    {
-        // rounds over this lane's true range, until tc symbols are out
-        const int32_t Tend = pos - 0;  // range upper end
-        (void)Tend;
-        const int32_t span = (int32_t)wave_max((uint32_t)(T0 - (j == 15 ? 0 : (int32_t)sDec.tstart[(lane + 1) & 63])));
-        const int32_t rounds = (span + kRoundBits - 1) / kRoundBits + 1;
-        for (int32_t r = 0; r < rounds; r++) {
-            const bool act = i < tc;
-            int32_t base = 0;
-            if (act) stage_round(src, pos, lane, base);
-            lds_sync();
-            if (act) {
-                StgBits sb;
-                sb_fill(sb, lane, pos - 8 * base);
-                const int32_t lo = pos - kRoundBits;
-                while (i < tc && pos > lo) {
-                    const uint32_t e = sb_huf(sb, lane, pos - 8 * base, tl);
-                    pos -= (int32_t)(e >> 8);
-                    acc |= (e & 0xFF) << (8 * (i & 3));
-                    i++;
-                    if ((i & 3) == 0) {
-                        gst<uint32_t>(out + i - 4, acc);
-                        acc = 0;
-                    }
-                }
+    // ---- phase 3: the synchronised speculative symbols into place
+    const uint32_t sk = sDec.skip[lane], from = sk, to = c;
+    const uint32_t o = sDec.obase[lane] + sDec.extra[lane];
+    if (to > from) {
+        if (to <= kSliceCap) {
+            uint32_t t = from;
+            for (; t + 4 <= to; t += 4) gst<uint32_t>(sdst + o + (t - from), gld<uint32_t>(slice + t));
+            for (; t < to; t++) gst<uint8_t>(sdst + o + (t - from), gb(slice + t));
+        } else {  // slice overflow: decode again from the synchronisation point
+            int32_t p = S - (int32_t)sDec.syncd[lane];
+            GBits g;
+            gbits_init(g, src, sl, p);
+            for (uint32_t t = from; t < to; t++) {
+                const uint32_t e = sDec.tab[gbits_peek(g, src, sl, p, tl)];
+                p -= (int32_t)(e >> 8);
+                gst<uint8_t>(sdst + o + (t - from), (uint8_t)e);
             }
-            lds_sync();
         }
-        for (uint32_t t = i & ~3u; t < i; t++) gst<uint8_t>(out + t, (uint8_t)(acc >> (8 * (t & 3))));
     }
     return true;
 }
@@ -456,6 +707,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
     dstCap = uni((uint64_t)dstCap);
     frameStart = uni((uint64_t)frameStart);
     S.lit = uni(S.lit);
+    S.htmp = uni(S.htmp);
     S.seqs = uni(S.seqs);
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
@@ -502,6 +754,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     dst = uni(dst);
     dstCap = uni((uint64_t)dstCap);
     S.lit = uni(S.lit);
+    S.htmp = uni(S.htmp);
     S.seqs = uni(S.seqs);
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
@@ -608,7 +861,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                         unsigned tlNew = 0;
                         const size_t hsz = huf_build_dtable_wave(hp, remain, &tlNew);
                         P.mark(1);
-                        if (hsz == 0) return z1::kDecErrCorrupt;
+                        if (hsz == 0) return z1::kDecErrHufTable;
                         hufValid = true;
                         hufTl = tlNew;
                         hp += hsz;
@@ -620,9 +873,9 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     if (single) {
                         if (lane == 0) ok = huf_decode1_lane(hufTl, hp, remain, litOut, (uint32_t)rs);
                     } else {
-                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs);
+                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, S.htmp);
                     }
-                    if (ballot(!ok)) return z1::kDecErrCorrupt;
+                    if (ballot(!ok)) return z1::kDecErrHufStream;
                     P.mark(2);
                 }
                 wave_sync();

@@ -18,6 +18,8 @@ enum DecErr : int {
     kDecErrCorrupt = -2,    // malformed block content
     kDecErrDstSmall = -3,   // output larger than the capacity given
     kDecErrSrcSmall = -4,   // truncated input
+    kDecErrHufTable = -5,   // malformed Huffman table description
+    kDecErrHufStream = -6,  // malformed Huffman stream
 };
 
 // ---------------------------------------------------------------------------------------------
