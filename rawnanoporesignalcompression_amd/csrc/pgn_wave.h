@@ -90,18 +90,18 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x)
     return x;
 }
 
-// one-wave workgroup barrier that also orders global/LDS memory for the wave's lanes
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }
-
-// LDS-only ordering point for a one-wave workgroup.  A wave's DS instructions are executed in order,
-// so lanes see each other's earlier LDS writes once the compiler keeps program order: a compiler
-// barrier suffices, and nothing waits on the wave's outstanding global loads/stores.
+// Ordering point between the lanes of a one-wave workgroup.  The lanes of a wavefront are coherent
+// through LDS and the CU's vector L1 without waits (a wave's DS and vector-memory instructions are
+// performed in program order; LLVM AMDGPU memory model, gfx942/gfx950), so keeping program order in
+// the compiler suffices.  In particular no s_waitcnt vmcnt(0): a __syncthreads() here would stall
+// every call site until the wave's outstanding HBM stores drain.
 __device__ __forceinline__ void lds_sync()
 {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_wave_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
+__device__ __forceinline__ void wave_sync() { lds_sync(); }
 
 // wave prefix sum of 64-bit values
 __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t x)

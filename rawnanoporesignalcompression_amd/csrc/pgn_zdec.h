@@ -448,7 +448,7 @@ __device__ __forceinline__ uint32_t walk_peek(int l, int32_t Sl, const uint8_t* 
 }
 
 __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                              uint8_t* htmp)
+                                              uint8_t* htmp, PhaseProf& P)
 {
     const int lane = lane_id();
     tl = uni(tl);
@@ -487,8 +487,10 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
 #pragma unroll
     for (int w = 0; w < kBmpBits / 32; w++) sDec.bmp[lane][w] = 0;
     uint8_t* slice = htmp + (size_t)lane * kSliceCap;
+    const uint32_t tmask = (1u << tl) - 1u;
     int32_t q = S;
-    uint32_t c = 0, acc = 0;
+    uint32_t stored = 0, npend = 0;  // symbols stored to the slice / held in pend
+    uint64_t pend = 0;
     {
         const int32_t rounds = (int32_t)wave_max((uint32_t)((S - E + kRoundBits - 1) / kRoundBits));
         uint4 nx[5];
@@ -507,31 +509,102 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             lds_sync();
             const int32_t lo = (hi - kRoundBits > E) ? hi - kRoundBits : E;
             const int32_t b8 = 8 * base;
-            while (q > lo) {
-                const int32_t d = S - q;
-                if (d < kBmpBits) atomicOr(&sDec.bmp[lane][d >> 5], 1u << (d & 31));
-                const uint32_t e = sDec.tab[stg_peek(lane, q - b8, tl)];
-                q -= (int32_t)(e >> 8);
-                acc |= (e & 0xFFu) << (8 * (c & 3));
-                c++;
-                if ((c & 3) == 0) {
-                    if (c <= kSliceCap) gst<uint32_t>(slice + c - 4, acc);
-                    acc = 0;
+            // register window: W = staged bits [wlo, wlo + 64), nxw = the word below it
+            int32_t wi = (q - b8 - (int32_t)tl) >> 5;
+            wi = wi < 0 ? 0 : (wi > kStgWords - 2 ? kStgWords - 2 : wi);
+            int32_t wlo = 32 * wi;
+            uint64_t W = (uint64_t)sDec.stg[lane][wi] | ((uint64_t)sDec.stg[lane][wi + 1] << 32);
+            uint32_t nxw = sDec.stg[lane][wi > 0 ? wi - 1 : 0];
+            auto step = [&](bool act) {
+                const int32_t x = q - b8 - (int32_t)tl;
+                const bool rf = x < wlo;
+                W = rf ? ((W << 32) | nxw) : W;
+                wlo = rf ? wlo - 32 : wlo;
+                nxw = sDec.stg[lane][wlo >= 64 ? (wlo >> 5) - 1 : 0];
+                const uint32_t e = sDec.tab[(uint32_t)(W >> ((x - wlo) & 63)) & tmask];
+                q = act ? q - (int32_t)(e >> 8) : q;
+                pend |= act ? ((uint64_t)(e & 0xFFu) << (8 * npend)) : 0ull;
+                npend += act ? 1u : 0u;
+            };
+            auto flush4 = [&]() {
+                if (npend >= 4) {
+                    if (stored + 4 <= kSliceCap) gst<uint32_t>(slice + stored, (uint32_t)pend);
+                    pend >>= 32;
+                    npend -= 4;
+                    stored += 4;
                 }
+            };
+            // the first kBmpBits bits below S: record every codeword boundary for the walk
+            while (q > lo && S - q < kBmpBits) {
+                const int32_t d = S - q;
+                atomicOr(&sDec.bmp[lane][d >> 5], 1u << (d & 31));
+                step(true);
+                flush4();
+            }
+            while (ballot(q > lo)) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) step(q > lo);
+                flush4();
             }
             lds_sync();
         }
-        if ((c & 3) && c <= kSliceCap)
-            for (uint32_t t = c & ~3u; t < c; t++) gst<uint8_t>(slice + t, (uint8_t)(acc >> (8 * (t & 3))));
+        for (uint32_t t = 0; t < npend; t++)
+            if (stored + t < kSliceCap) gst<uint8_t>(slice + stored + t, (uint8_t)(pend >> (8 * t)));
     }
+    const uint32_t c = stored + npend;
+    P.mark(11);
     sDec.cnt[lane] = c;
     sDec.startp[lane] = (uint32_t)S;
     sDec.endp[lane] = (uint32_t)E;
     sDec.exitp[lane] = (uint32_t)q;
     lds_sync();
-    // ---- phase 2: walk the true path across the borders (one lane per stream)
+    // ---- phase 2: the border walks.  If lane l-1 synchronised, the true path enters lane l's range
+    // at l-1's speculative exit, so all 15 walks of a stream run at once; the walk symbols wait in
+    // the (now free) staging row.  A stream with a lane that does not meet its boundaries within
+    // kBmpBits bits falls back to the serial walker.
+    uint8_t* wsym = (uint8_t*)sDec.stg[lane];
+    constexpr uint32_t kWalkMax = 4 * kStgWords;
+    uint32_t ex = 0;
+    int32_t p = (j == 0) ? S : (int32_t)sDec.exitp[lane - 1];
+    bool synced = (j == 0);
+    if (j > 0) {
+        while (p > E && ex < kWalkMax) {
+            const int32_t d = S - p;
+            if (d >= kBmpBits) break;
+            if ((sDec.bmp[lane][d >> 5] >> (d & 31)) & 1u) { synced = true; break; }
+            const uint32_t e = sDec.tab[walk_peek(lane, S, src, sl, p, tl)];
+            p -= (int32_t)(e >> 8);
+            wsym[ex++] = (uint8_t)e;
+        }
+    }
+    const int32_t dsync = S - p;
+    uint32_t idx = 0;
+    if (synced && j > 0) {
+        for (int w = 0; w < (dsync >> 5); w++) idx += (uint32_t)__builtin_popcount(sDec.bmp[lane][w]);
+        if (dsync & 31) idx += (uint32_t)__builtin_popcount(sDec.bmp[lane][dsync >> 5] & ((1u << (dsync & 31)) - 1u));
+    }
+    const uint64_t unsynced = ballot(!synced);
+    const bool fast = ((unsynced >> (16 * k)) & 0xFFFFull) == 0;
     uint8_t* sdst = dst + (size_t)seg * (size_t)k;
-    if (j == 0) {
+    if (fast) {
+        const uint32_t tc = ex + (c - idx);
+        uint32_t incl = tc;  // inclusive sum over the stream's 16 lanes (one DPP row)
+        incl += dpp<kDppRowShr1>(incl);
+        incl += dpp<kDppRowShr2>(incl);
+        incl += dpp<kDppRowShr4>(incl);
+        incl += dpp<kDppRowShr8>(incl);
+        sDec.skip[lane] = idx;
+        sDec.syncd[lane] = (uint32_t)dsync;
+        sDec.extra[lane] = ex;
+        sDec.obase[lane] = incl - tc;
+        if (j == 15) {
+            sDec.u[8 + k] = incl;
+            sDec.u[12 + k] = (uint32_t)q;  // true end of the stream (must be 0)
+        }
+    }
+    lds_sync();
+    // serial fallback: one lane per stream walks the 15 borders in order
+    if (!fast && j == 0) {
         sDec.skip[lane] = 0;
         sDec.syncd[lane] = 0;
         sDec.extra[lane] = 0;
@@ -543,63 +616,76 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             const uint32_t cl = sDec.cnt[l];
             const int32_t Sl = (int32_t)sDec.startp[l], El = (int32_t)sDec.endp[l];
             sDec.obase[l] = out;
-            int32_t p = T;
-            uint32_t ex = 0;
-            bool synced = false;
-            while (p > El) {
-                const int32_t d = Sl - p;
+            int32_t pp = T;
+            uint32_t exx = 0;
+            bool sy = false;
+            while (pp > El) {
+                const int32_t d = Sl - pp;
                 if (d >= kBmpBits) break;  // past the recorded boundaries: finish serially below
-                if ((sDec.bmp[l][d >> 5] >> (d & 31)) & 1u) { synced = true; break; }
-                const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, p, tl)];
-                p -= (int32_t)(e >> 8);
-                if (out + ex < nsym) gst<uint8_t>(sdst + out + ex, (uint8_t)e);
-                ex++;
+                if ((sDec.bmp[l][d >> 5] >> (d & 31)) & 1u) { sy = true; break; }
+                const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, pp, tl)];
+                pp -= (int32_t)(e >> 8);
+                if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
+                exx++;
             }
-            if (synced) {
-                // speculative symbols before the meeting point: boundaries recorded above it
-                const int32_t d = Sl - p;
-                uint32_t idx = 0;
-                for (int w = 0; w < (d >> 5); w++) idx += (uint32_t)__builtin_popcount(sDec.bmp[l][w]);
-                if (d & 31) idx += (uint32_t)__builtin_popcount(sDec.bmp[l][d >> 5] & ((1u << (d & 31)) - 1u));
-                sDec.skip[l] = idx;
+            if (sy) {
+                const int32_t d = Sl - pp;
+                uint32_t ix = 0;
+                for (int w = 0; w < (d >> 5); w++) ix += (uint32_t)__builtin_popcount(sDec.bmp[l][w]);
+                if (d & 31) ix += (uint32_t)__builtin_popcount(sDec.bmp[l][d >> 5] & ((1u << (d & 31)) - 1u));
+                sDec.skip[l] = ix;
                 sDec.syncd[l] = (uint32_t)d;
                 T = (int32_t)sDec.exitp[l];
-                out += ex + (cl - idx);
+                out += exx + (cl - ix);
             } else {  // no common boundary: the walker decodes the rest of the range itself
-                while (p > El) {
-                    const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, p, tl)];
-                    p -= (int32_t)(e >> 8);
-                    if (out + ex < nsym) gst<uint8_t>(sdst + out + ex, (uint8_t)e);
-                    ex++;
+                while (pp > El) {
+                    const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, pp, tl)];
+                    pp -= (int32_t)(e >> 8);
+                    if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
+                    exx++;
                 }
                 sDec.skip[l] = cl;
-                T = p;
-                out += ex;
+                T = pp;
+                out += exx;
             }
-            sDec.extra[l] = ex;
+            sDec.extra[l] = exx;
         }
-        sDec.u[12 + k] = (uint32_t)T;    // true end of the stream (must be 0)
-        sDec.u[8 + k] = out;             // symbols of the stream
+        sDec.u[12 + k] = (uint32_t)T;
+        sDec.u[8 + k] = out;
     }
     lds_sync();
+    P.mark(12);
     const bool good = (sDec.u[8 + k] == nsym) && ((int32_t)sDec.u[12 + k] == 0);
     if (ballot(!good)) return false;
-    // ---- phase 3: the synchronised speculative symbols into place
-    const uint32_t sk = sDec.skip[lane], from = sk, to = c;
-    const uint32_t o = sDec.obase[lane] + sDec.extra[lane];
-    if (to > from) {
-        if (to <= kSliceCap) {
-            uint32_t t = from;
-            for (; t + 4 <= to; t += 4) gst<uint32_t>(sdst + o + (t - from), gld<uint32_t>(slice + t));
-            for (; t < to; t++) gst<uint8_t>(sdst + o + (t - from), gb(slice + t));
+    // ---- phase 3: walk symbols and the synchronised speculative symbols into place
+    const uint32_t sk = sDec.skip[lane];
+    const uint32_t ob = sDec.obase[lane], exl = sDec.extra[lane];
+    if (fast)
+        for (uint32_t t = 0; t < exl; t++) gst<uint8_t>(sdst + ob + t, wsym[t]);
+    const uint32_t o = ob + exl;
+    if (c > sk) {
+        const uint32_t len = c - sk;
+        if (c <= kSliceCap) {
+            const uint8_t* from = slice + sk;
+            uint8_t* to = sdst + o;
+            uint32_t t = 0;
+            for (; t + 64 <= len; t += 64) {
+                uint4 v[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) v[u] = gld<uint4>(from + t + 16 * u);
+#pragma unroll
+                for (int u = 0; u < 4; u++) gst<uint4>(to + t + 16 * u, v[u]);
+            }
+            for (; t + 4 <= len; t += 4) gst<uint32_t>(to + t, gld<uint32_t>(from + t));
+            for (; t < len; t++) gst<uint8_t>(to + t, gb(from + t));
         } else {  // slice overflow: decode again from the synchronisation point
-            int32_t p = S - (int32_t)sDec.syncd[lane];
+            int32_t pp = S - (int32_t)sDec.syncd[lane];
             GBits g;
-            gbits_init(g, src, sl, p);
-            for (uint32_t t = from; t < to; t++) {
-                const uint32_t e = sDec.tab[gbits_peek(g, src, sl, p, tl)];
-                p -= (int32_t)(e >> 8);
-                gst<uint8_t>(sdst + o + (t - from), (uint8_t)e);
+            gbits_init(g, src, sl, pp);
+            for (uint32_t t = 0; t < len; t++) {
+                const uint32_t e = sDec.tab[gbits_peek(g, src, sl, pp, tl)];
+                pp -= (int32_t)(e >> 8);
+                gst<uint8_t>(sdst + o + t, (uint8_t)e);
             }
         }
     }
@@ -873,7 +959,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     if (single) {
                         if (lane == 0) ok = huf_decode1_lane(hufTl, hp, remain, litOut, (uint32_t)rs);
                     } else {
-                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, S.htmp);
+                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, S.htmp, P);
                     }
                     if (ballot(!ok)) return z1::kDecErrHufStream;
                     P.mark(2);

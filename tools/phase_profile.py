@@ -12,8 +12,8 @@ from rawnanoporesignalcompression_amd import PGNanoCodec
 
 ENC = ["split", "search", "lit_gather", "hist", "sort", "tree+hdr(lane0)", "huf_encode", "raw_lit", "seq(lane0)",
        "frame_finish"]
-DEC = ["parse/merge_wait", "huf_table(lane0)", "huf_decode", "seq_list(lane0)", "seq_exec", "raw_copy", "merge",
-       "lit_hdr"]
+DEC = ["parse/merge_wait", "huf_table", "huf_copy(ph3)", "seq_list", "seq_exec", "raw_copy", "merge",
+       "lit_hdr", "-", "-", "-", "huf_spec(ph1)", "huf_walk(ph2)"]
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 S = 100000
 c = PGNanoCodec(0)
