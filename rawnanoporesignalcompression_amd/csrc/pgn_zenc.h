@@ -14,7 +14,7 @@
 
 namespace pgn {
 
-constexpr int kWinWords = 200;  // 512 symbols * 12 bits / 32 + carry
+constexpr int kWinWords = 392;  // 1024 symbols * 12 bits / 32 + carry words
 constexpr int kFiltSlots = 1024;  // match-search round filter (64 lanes x 2 hashes)
 
 // FSE compression table of the Huffman weight alphabet (<= 13 symbols, tableLog <= 6)
@@ -52,6 +52,16 @@ struct EncLds {
             uint32_t wcount[16];  // weight histogram
             int16_t wnorm[16];
             uint32_t wcumul[16];
+        };
+        struct {  // sequences section (after the literals section is written)
+            z1::FseCTable sct[3];  // ll, of, ml
+            uint8_t stsym[512];    // FSE spread scratch
+            uint32_t scount[3][64];
+            int16_t snorm[64];
+            uint32_t scumul[64];
+            uint8_t snc[128];      // normalized-count header staging
+            uint32_t sv[3][64];    // staged sequences: litLength, mlBase, offset
+            uint8_t sc[3][64];     //                   ll, of, ml codes
         };
     };
     uint32_t u[8];
@@ -306,81 +316,101 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
 
 // ---------------------------------------------------------------------------------------------
 // Huffman bit packing of one segment: symbols are written last-to-first (HUF_compress1X order), so
-// the stream position of a symbol is the sum of the code lengths of the symbols after it.
+// emission r takes symbol src[len-1-r] and its bit position is the sum of the code lengths emitted
+// before it.  A step emits 1024 symbols, 16 per lane from one 16-byte load; lane code groups are
+// OR-ed into an LDS bit window at their prefix-sum offsets, and the window's complete words leave
+// as coalesced dword stores.
 // ---------------------------------------------------------------------------------------------
 __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, const uint8_t* __restrict__ src, uint32_t len,
                                                      uint32_t totalBits)
 {
-    const int lane = lane_id();
+    const uint32_t lane = (uint32_t)lane_id();
     out = uni(out);
     src = uni(src);
     len = uni(len);
     totalBits = uni(totalBits);
     const uint32_t* cw = sEnc.cw;
     uint32_t* win = sEnc.win;
-    for (int w = lane; w < kWinWords; w += 64) win[w] = 0;
-    wave_sync();
+    for (uint32_t w = lane; w < (uint32_t)kWinWords; w += 64) win[w] = 0;
+    lds_sync();
     uint32_t winLo = 0;   // bit offset of win[0] (multiple of 32)
     uint32_t bitBase = 0; // bits emitted before this step
-    for (uint32_t r0 = 0; r0 < len; r0 += 512) {
-        uint32_t code[8], nb[8];
+    for (uint32_t r0 = 0; r0 < len; r0 += 1024) {
+        // my 16 emissions r0 + 16*lane + j are bytes len-1-r of src: one 16-byte block, reversed
+        const int32_t a = (int32_t)len - 16 - (int32_t)(r0 + 16 * lane);
+        uint32_t wv[4];
+        if (a >= 0) {
+            const uint4 v = gld<uint4>(src + a);
+            wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t x = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    const int32_t i = a + 4 * q + b;
+                    if (i >= 0) x |= (uint32_t)gb(src + i) << (8 * b);
+                }
+                wv[q] = x;
+            }
+        }
+        const int32_t nvalid = (int32_t)len - (int32_t)(r0 + 16 * lane);  // emissions of mine (may be <= 0 or > 16)
+        uint64_t grp[4];
+        uint32_t gnb[4];
         uint32_t myBits = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            uint32_t r = r0 + (uint32_t)lane * 8 + (uint32_t)j;
-            nb[j] = 0;
-            code[j] = 0;
-            if (r < len) {
-                uint32_t c = cw[gb(src + len - 1 - r)];
-                code[j] = c & 0xFFFF;
-                nb[j] = c >> 16;
+        for (int g = 0; g < 4; g++) {
+            uint64_t acc = 0;
+            uint32_t n = 0;
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const int j = 4 * g + jj;
+                const uint32_t sym = (wv[(15 - j) >> 2] >> (8 * ((15 - j) & 3))) & 0xFFu;
+                const uint32_t cwj = (j < nvalid) ? cw[sym] : 0u;
+                acc |= (uint64_t)(cwj & 0xFFFFu) << n;
+                n += cwj >> 16;
             }
-            myBits += nb[j];
+            grp[g] = acc;
+            gnb[g] = n;
+            myBits += n;
         }
         const uint32_t incl = wave_incl_sum(myBits);
         const uint32_t stepBits = readlane_u32(incl, 63);
         uint32_t pos = bitBase + (incl - myBits) - winLo;  // window-relative bit position
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            uint64_t acc = 0;
-            uint32_t n = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                acc |= (uint64_t)code[4 * h + j] << n;
-                n += nb[4 * h + j];
-            }
+        for (int g = 0; g < 4; g++) {
+            const uint32_t n = gnb[g];
             if (n) {
-                uint32_t w = pos >> 5, sh = pos & 31;
-                uint64_t lo = acc << sh;
+                const uint32_t w = pos >> 5, sh = pos & 31;
+                const uint64_t lo = grp[g] << sh;
                 atomicOr(&win[w], (uint32_t)lo);
                 if (sh + n > 32) atomicOr(&win[w + 1], (uint32_t)(lo >> 32));
-                if (sh + n > 64) atomicOr(&win[w + 2], (uint32_t)(acc >> (64 - sh)));
+                if (sh + n > 64) atomicOr(&win[w + 2], (uint32_t)(grp[g] >> (64 - sh)));
             }
             pos += n;
         }
-        wave_sync();
+        lds_sync();
         const uint32_t endRel = bitBase + stepBits - winLo;
         const uint32_t complete = endRel >> 5;
         uint8_t* o = out + (winLo >> 3);
-        for (uint32_t w = (uint32_t)lane; w < complete; w += 64) gst<uint32_t>(o + 4 * w, win[w]);
+        for (uint32_t w = lane; w < complete; w += 64) gst<uint32_t>(o + 4 * w, win[w]);
         const uint32_t carry = win[complete];
-        wave_sync();
-        for (uint32_t w = (uint32_t)lane; w <= complete + 3 && w < (uint32_t)kWinWords; w += 64) win[w] = 0;
-        wave_sync();
-        if (lane == 0) win[0] = carry;
+        lds_sync();
+        for (uint32_t w = lane; w <= complete; w += 64) win[w] = (w == 0) ? carry : 0u;
+        lds_sync();
         winLo += complete * 32;
         bitBase += stepBits;
-        wave_sync();
     }
     // end mark, then the last partial bytes
     if (lane == 0) {
-        uint32_t rel = totalBits - winLo;
+        const uint32_t rel = totalBits - winLo;
         win[rel >> 5] |= 1u << (rel & 31);
-        uint32_t nbytes = ((totalBits + 8) >> 3) - (winLo >> 3);
-        uint8_t* o = out + (winLo >> 3);
-        for (uint32_t b = 0; b < nbytes; b++) gst<uint8_t>(o + b, (uint8_t)(win[b >> 2] >> (8 * (b & 3))));
     }
-    wave_sync();
+    lds_sync();
+    const uint32_t nbytes = ((totalBits + 8) >> 3) - (winLo >> 3);
+    uint8_t* o = out + (winLo >> 3);
+    for (uint32_t b = lane; b < nbytes; b += 64) gst<uint8_t>(o + b, (uint8_t)(win[b >> 2] >> (8 * (b & 3))));
+    lds_sync();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -777,14 +807,243 @@ __device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t
     return (maxSym + 1) / 2 + 1;
 }
 
-// lane 0: the sequences section into the staging buffer (rare on nanopore streams)
-__device__ __noinline__ void seq_section_lane0(EncScratch S, uint32_t nbSeq)
+// ---------------------------------------------------------------------------------------------
+// Sequences section (ZSTD_compressSequences_internal, repeat mode none; zstd1_model.h
+// compress_sequences): codes and their histograms in parallel over the sequences, table choice and
+// FSE tables wave-uniform in LDS, then the serial backward encode over sequences staged 64 at a
+// time into LDS.  Writes S.seqSection; returns its size, or (size_t)-1 / -2 for "emit a raw block".
+// ---------------------------------------------------------------------------------------------
+// FSE_buildCTable_wksp, wave-uniform, cumul / tableSymbol in LDS
+__device__ __forceinline__ void fse_build_ctable_lds(z1::FseCTable& ct, const int16_t* norm, unsigned maxSymbolValue,
+                                                     unsigned tableLog, uint8_t* tableSymbol, uint32_t* cumul)
+{
+    const uint32_t tableSize = 1u << tableLog;
+    const uint32_t tableMask = tableSize - 1;
+    const uint32_t step = (tableSize >> 1) + (tableSize >> 3) + 3;
+    uint32_t highThreshold = tableSize - 1;
+    ct.tableLog = tableLog;
+    cumul[0] = 0;
+    for (unsigned u = 1; u <= maxSymbolValue + 1; u++) {
+        if (norm[u - 1] == -1) {
+            cumul[u] = cumul[u - 1] + 1;
+            tableSymbol[highThreshold--] = (uint8_t)(u - 1);
+        } else {
+            cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
+        }
+    }
+    cumul[maxSymbolValue + 1] = tableSize + 1;
+    uint32_t position = 0;
+    for (unsigned symbol = 0; symbol <= maxSymbolValue; symbol++) {
+        const int freq = norm[symbol];
+        for (int k = 0; k < freq; k++) {
+            tableSymbol[position] = (uint8_t)symbol;
+            position = (position + step) & tableMask;
+            while (position > highThreshold) position = (position + step) & tableMask;
+        }
+    }
+    lds_sync();
+    for (uint32_t u = 0; u < tableSize; u++) {
+        const uint8_t sy = tableSymbol[u];
+        const uint32_t cs = cumul[sy];
+        ct.stateTable[cs] = (uint16_t)(tableSize + u);
+        cumul[sy] = cs + 1;
+    }
+    unsigned total = 0;
+    for (unsigned sy = 0; sy <= maxSymbolValue; sy++) {
+        const int nv = norm[sy];
+        if (nv == 0) {
+            ct.deltaNbBits[sy] = ((tableLog + 1) << 16) - (1u << tableLog);
+            ct.deltaFindState[sy] = 0;
+        } else if (nv == -1 || nv == 1) {
+            ct.deltaNbBits[sy] = (tableLog << 16) - (1u << tableLog);
+            ct.deltaFindState[sy] = (int32_t)total - 1;
+            total++;
+        } else {
+            const uint32_t maxBitsOut = tableLog - z1::highbit32((uint32_t)(nv - 1));
+            const uint32_t minStatePlus = (uint32_t)nv << maxBitsOut;
+            ct.deltaNbBits[sy] = (maxBitsOut << 16) - minStatePlus;
+            ct.deltaFindState[sy] = (int32_t)total - nv;
+            total += (unsigned)nv;
+        }
+    }
+    lds_sync();
+}
+
+// little-endian bit writer into global memory, 32-bit flushes (byte-exact with z1::BitW)
+struct GBitW {
+    uint8_t* p;
+    uint64_t acc;
+    uint32_t n;
+};
+__device__ __forceinline__ void gbw_add(GBitW& b, uint32_t v, uint32_t nb)
+{
+    b.acc |= (uint64_t)(v & (uint32_t)((1ull << nb) - 1ull)) << b.n;
+    b.n += nb;
+    if (b.n >= 32) {
+        if (lane_id() == 0) gst<uint32_t>(b.p, (uint32_t)b.acc);
+        b.p += 4;
+        b.acc >>= 32;
+        b.n -= 32;
+    }
+}
+__device__ __forceinline__ size_t gbw_close(GBitW& b, const uint8_t* start)
+{
+    gbw_add(b, 1, 1);
+    const uint32_t nbytes = (b.n + 7) >> 3;
+    if (lane_id() == 0)
+        for (uint32_t i = 0; i < nbytes; i++) gst<uint8_t>(b.p + i, (uint8_t)(b.acc >> (8 * i)));
+    return (size_t)(b.p + nbytes - start);
+}
+__device__ __forceinline__ void sfse_init(uint32_t& st, const z1::FseCTable& ct, unsigned symbol)
+{
+    const uint32_t nbBitsOut = (ct.deltaNbBits[symbol] + (1u << 15)) >> 16;
+    const uint32_t v = (nbBitsOut << 16) - ct.deltaNbBits[symbol];
+    st = ct.stateTable[(v >> nbBitsOut) + ct.deltaFindState[symbol]];
+}
+__device__ __forceinline__ void sfse_encode(GBitW& bw, uint32_t& st, const z1::FseCTable& ct, unsigned symbol)
+{
+    const uint32_t nbBitsOut = (st + ct.deltaNbBits[symbol]) >> 16;
+    gbw_add(bw, st, nbBitsOut);
+    st = ct.stateTable[(st >> nbBitsOut) + ct.deltaFindState[symbol]];
+}
+
+__device__ __noinline__ size_t seq_section_wave(EncScratch S, uint32_t nbSeq)
 {
     EncLds& L = sEnc;
-    size_t r = z1::compress_sequences(S.seqSection, S.seqs, nbSeq, S.codes, S.codes + S.maxSeq, S.codes + 2 * S.maxSeq,
-                                      *S.seqWork);
-    L.u[2] = (uint32_t)r;
-    L.u[3] = (r == (size_t)-1 || r == (size_t)-2) ? 1u : 0u;
+    const uint32_t lane = (uint32_t)lane_id();
+    nbSeq = uni(nbSeq);
+    S.seqs = uni(S.seqs);
+    S.codes = uni(S.codes);
+    S.seqSection = uni(S.seqSection);
+    S.maxSeq = uni(S.maxSeq);
+    uint8_t* const dst = S.seqSection;
+    uint8_t* llC = S.codes;
+    uint8_t* ofC = S.codes + S.maxSeq;
+    uint8_t* mlC = S.codes + 2 * S.maxSeq;
+    const uint32_t* sq = (const uint32_t*)S.seqs;  // {litLength, offset, mlBase} per sequence
+    // number of sequences
+    uint32_t hl;
+    if (nbSeq < 128) {
+        if (lane == 0) gst<uint8_t>(dst, (uint8_t)nbSeq);
+        hl = 1;
+    } else if (nbSeq < 0x7F00) {
+        if (lane == 0) { gst<uint8_t>(dst, (uint8_t)((nbSeq >> 8) + 0x80)); gst<uint8_t>(dst + 1, (uint8_t)nbSeq); }
+        hl = 2;
+    } else {
+        if (lane == 0) { gst<uint8_t>(dst, 0xFF); gst<uint8_t>(dst + 1, (uint8_t)(nbSeq - 0x7F00)); gst<uint8_t>(dst + 2, (uint8_t)((nbSeq - 0x7F00) >> 8)); }
+        hl = 3;
+    }
+    if (nbSeq == 0) return hl;
+    uint8_t* const seqHead = dst + hl;
+    uint8_t* op = seqHead + 1;
+    // codes and histograms
+    for (int k = 0; k < 3; k++) L.scount[k][lane] = 0;
+    lds_sync();
+    for (uint32_t i = lane; i < nbSeq; i += 64) {
+        const uint32_t litLength = gld<uint32_t>(sq + 3 * i), offset = gld<uint32_t>(sq + 3 * i + 1),
+                       mlBase = gld<uint32_t>(sq + 3 * i + 2);
+        const uint32_t lc = z1::ll_code(litLength), oc = z1::highbit32(offset), mc = z1::ml_code(mlBase);
+        gst<uint8_t>(llC + i, (uint8_t)lc);
+        gst<uint8_t>(ofC + i, (uint8_t)oc);
+        gst<uint8_t>(mlC + i, (uint8_t)mc);
+        atomicAdd(&L.scount[0][lc], 1u);
+        atomicAdd(&L.scount[1][oc], 1u);
+        atomicAdd(&L.scount[2][mc], 1u);
+    }
+    lds_sync();
+    const uint32_t last = nbSeq - 1;
+    const uint32_t lastLL = gld<uint32_t>(sq + 3 * last), lastOff = gld<uint32_t>(sq + 3 * last + 1),
+                   lastML = gld<uint32_t>(sq + 3 * last + 2);
+    const uint32_t lastCode[3] = {z1::ll_code(lastLL), z1::highbit32(lastOff), z1::ml_code(lastML)};
+    uint8_t* lastNCount = nullptr;
+    uint32_t types[3];
+    const unsigned maxes[3] = {z1::kMaxLL, z1::kMaxOff, z1::kMaxML};
+    const unsigned fseLogs[3] = {z1::kLLFSELog, z1::kOffFSELog, z1::kMLFSELog};
+    const unsigned normLogs[3] = {z1::kLLDefaultNormLog, z1::kOFDefaultNormLog, z1::kMLDefaultNormLog};
+    const unsigned defMax[3] = {z1::kMaxLL, z1::kDefaultMaxOff, z1::kMaxML};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const uint32_t cnt = (lane <= maxes[k]) ? L.scount[k][lane] : 0u;
+        const uint64_t nz = ballot(cnt != 0);
+        const unsigned mx = 63u - (unsigned)__builtin_clzll(nz);
+        const uint32_t mostFrequent = wave_max(cnt);
+        const bool defaultAllowed = (k == 1) ? (mx <= z1::kDefaultMaxOff) : true;
+        const unsigned type = z1::select_encoding_type(mostFrequent, nbSeq, normLogs[k], defaultAllowed);
+        types[k] = type;
+        z1::FseCTable& ct = L.sct[k];
+        if (type == z1::kSetRle) {
+            ct.tableLog = 0;
+            ct.stateTable[0] = 0;
+            ct.stateTable[1] = 0;
+            ct.deltaNbBits[mx] = 0;
+            ct.deltaFindState[mx] = 0;
+            if (lane == 0) gst<uint8_t>(op, (uint8_t)lastCode[k]);
+            op += 1;
+        } else if (type == z1::kSetBasic) {
+            if (lane <= defMax[k])
+                L.snorm[lane] = k == 0 ? z1::ll_default_norm(lane) : (k == 1 ? z1::of_default_norm(lane) : z1::ml_default_norm(lane));
+            lds_sync();
+            fse_build_ctable_lds(ct, L.snorm, defMax[k], normLogs[k], L.stsym, L.scumul);
+        } else {
+            size_t nbSeq_1 = nbSeq;
+            const unsigned tableLog = z1::fse_optimal_table_log(fseLogs[k], nbSeq, mx, 2);
+            if (L.scount[k][lastCode[k]] > 1) {
+                L.scount[k][lastCode[k]] -= 1;
+                nbSeq_1--;
+            }
+            lds_sync();
+            if (!z1::fse_normalize(L.snorm, tableLog, L.scount[k], nbSeq_1, mx, nbSeq_1 >= 2048)) return (size_t)-2;
+            lds_sync();
+            const size_t nc = z1::fse_write_ncount(L.snc, L.snorm, mx, tableLog);
+            if (nc == 0) return (size_t)-2;
+            lds_sync();
+            for (uint32_t i = lane; i < nc; i += 64) gst<uint8_t>(op + i, L.snc[i]);
+            fse_build_ctable_lds(ct, L.snorm, mx, tableLog, L.stsym, L.scumul);
+            lastNCount = op;
+            op += nc;
+        }
+        lds_sync();
+    }
+    if (lane == 0) gst<uint8_t>(seqHead, (uint8_t)((types[0] << 6) + (types[1] << 4) + (types[2] << 2)));
+    // ZSTD_encodeSequences (no long offsets: windowLog <= 17), backwards
+    GBitW bw{op, 0, 0};
+    uint32_t sLL, sOF, sML;
+    sfse_init(sML, L.sct[2], lastCode[2]);
+    sfse_init(sOF, L.sct[1], lastCode[1]);
+    sfse_init(sLL, L.sct[0], lastCode[0]);
+    gbw_add(bw, lastLL, z1::ll_bits(lastCode[0]));
+    gbw_add(bw, lastML, z1::ml_bits(lastCode[2]));
+    gbw_add(bw, lastOff, lastCode[1]);
+    for (int32_t blk = (int32_t)(last - 1) >> 6; blk >= 0 && last > 0; blk--) {
+        const uint32_t i = 64u * (uint32_t)blk + lane;
+        lds_sync();
+        if (i < last) {
+            L.sv[0][lane] = gld<uint32_t>(sq + 3 * i);
+            L.sv[1][lane] = gld<uint32_t>(sq + 3 * i + 2);
+            L.sv[2][lane] = gld<uint32_t>(sq + 3 * i + 1);
+            L.sc[0][lane] = gb(llC + i);
+            L.sc[1][lane] = gb(ofC + i);
+            L.sc[2][lane] = gb(mlC + i);
+        }
+        lds_sync();
+        const int32_t top = (64 * blk + 63 < (int32_t)last - 1) ? 63 : (int32_t)last - 1 - 64 * blk;
+        for (int32_t t = top; t >= 0; t--) {
+            const uint32_t lc = L.sc[0][t], oc = L.sc[1][t], mc = L.sc[2][t];
+            sfse_encode(bw, sOF, L.sct[1], oc);
+            sfse_encode(bw, sML, L.sct[2], mc);
+            sfse_encode(bw, sLL, L.sct[0], lc);
+            gbw_add(bw, L.sv[0][t], z1::ll_bits(lc));
+            gbw_add(bw, L.sv[1][t], z1::ml_bits(mc));
+            gbw_add(bw, L.sv[2][t], oc);
+        }
+    }
+    gbw_add(bw, sML, L.sct[2].tableLog);
+    gbw_add(bw, sOF, L.sct[1].tableLog);
+    gbw_add(bw, sLL, L.sct[0].tableLog);
+    const size_t streamSize = gbw_close(bw, op);
+    op += streamSize;
+    if (lastNCount && (op - lastNCount) < 4) return (size_t)-1;
+    return (size_t)(op - dst);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -989,9 +1248,8 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         if (lane == 0) body[litSize] = 0;
         seqSize = 1;
     } else {
-        if (lane == 0) seq_section_lane0(S, nbSeq);
-        wave_sync();
-        seqSize = L.u[3] ? (size_t)-1 : (size_t)L.u[2];
+        const size_t r = seq_section_wave(S, nbSeq);
+        seqSize = (r == (size_t)-1 || r == (size_t)-2) ? (size_t)-1 : r;
         P.mark(8);
     }
     const size_t maxCSize = n - ((n >> 6) + 2);
