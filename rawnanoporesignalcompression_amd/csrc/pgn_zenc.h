@@ -421,7 +421,7 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
 // codes from ballots.  Writes L.nbBits / L.val per symbol; returns the largest code length.
 // nnz = number of symbols with a nonzero count (>= 2).
 // ---------------------------------------------------------------------------------------------
-__device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBits, uint32_t nnz)
+__device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBits, uint32_t nnz, PhaseProf& P)
 {
     EncLds& L = sEnc;
     const int lane = lane_id();
@@ -472,6 +472,7 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
         nodeNb++;
     }
     lds_sync();
+    P.mark(11);
     // ---- depths of the internal nodes: pointer jumping (distance to ancestor, ancestor of ancestor)
     uint32_t anc[4], dep[4];
 #pragma unroll
@@ -523,6 +524,7 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
         }
     }
     lds_sync();
+    P.mark(12);
     // ---- HUF_setMaxHeight
     const uint32_t largestBits = hn[nonNullRank].nbBits;
     if (largestBits > maxNbBits) {
@@ -603,6 +605,7 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
     } else {
         maxNbBits = largestBits;
     }
+    P.mark(13);
     // ---- canonical codes: starting value per length, then symbol order within a length
     {
         uint32_t mn = 0;
@@ -717,7 +720,7 @@ __device__ __forceinline__ void wfse_encode(z1::BitW& bw, uint32_t& st, const WC
 
 // HUF_writeCTable into L.hdr from L.nbBits (wave-uniform; weights and their histogram by ballots).
 // Returns the description size, 0 if it cannot be written (raw weights with > 128 symbols).
-__device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t huffLog)
+__device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t huffLog, PhaseProf& P)
 {
     EncLds& L = sEnc;
     const int lane = lane_id();
@@ -1144,8 +1147,9 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     uint32_t nnz = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) nnz += (uint32_t)__builtin_popcountll(ballot(c[q] != 0));
-    const uint32_t hl = huf_tree_wave(maxSym, huffLog, nnz);
-    const uint32_t hSize = huf_write_ctable_wave(maxSym, hl);
+    const uint32_t hl = huf_tree_wave(maxSym, huffLog, nnz, P);
+    P.mark(14);
+    const uint32_t hSize = huf_write_ctable_wave(maxSym, hl, P);
     P.mark(5);
     if (hSize == 0 || hSize + 12 >= n) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     // exact stream sizes from the segment histograms
