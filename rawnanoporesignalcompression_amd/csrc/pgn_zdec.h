@@ -18,9 +18,10 @@ constexpr int kBndBelow = 20;
 
 struct DecLds {
     uint16_t tab[1 << z1::kHufTableLogMax];  // Huffman decode table: symbol | nbBits << 8
-    uint32_t bmp[64][kBmpBits / 32];         // speculative decode: boundary bitmap below each lane start
-    uint32_t stg[64][kStgWords];             // staged stream bytes of the current round, per lane
-    uint8_t bnd[64][kBnd];                   // bytes around each lane's start (phase-2 walk)
+    // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
+    uint32_t bmp[kBmpBits / 32][64];         // speculative decode: boundary bitmap below each lane start
+    uint32_t stg[kStgWords][64];             // staged stream bytes of the current round
+    uint32_t bnd[kBnd / 4][64];              // bytes around each lane's start (phase-2 walk), word-major
     uint32_t cnt[64], startp[64], endp[64], exitp[64], skip[64], extra[64], obase[64], syncd[64];
     uint8_t wts[256];                        // weights of the current table
     uint8_t order[256];                      // symbols sorted by (weight, symbol)
@@ -138,7 +139,7 @@ __device__ __forceinline__ uint32_t stg_peek(int lane, int32_t x, unsigned tl)
 {
     const int32_t lo = x - (int32_t)tl;
     const int32_t w = lo >> 5;
-    const uint64_t v = (uint64_t)sDec.stg[lane][w] | ((uint64_t)sDec.stg[lane][w + 1] << 32);
+    const uint64_t v = (uint64_t)sDec.stg[w][lane] | ((uint64_t)sDec.stg[w + 1][lane] << 32);
     return (uint32_t)(v >> (lo & 31)) & ((1u << tl) - 1u);
 }
 
@@ -421,6 +422,8 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
 // point are written by the walker.  Finally every lane copies its synchronised symbols into place
 // (phase 3).  Returns false on a malformed stream.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint8_t bnd_byte(int l, int32_t b) { return ((const uint8_t*)&sDec.bnd[b >> 2][l])[b & 3]; }
+
 // the walker's bit peek: from the lane's cached border bytes when they cover [q - tl, q)
 __device__ __forceinline__ uint32_t walk_peek(int l, int32_t Sl, const uint8_t* s, int32_t sl, int32_t q, unsigned tl)
 {
@@ -437,7 +440,7 @@ __device__ __forceinline__ uint32_t walk_peek(int l, int32_t Sl, const uint8_t* 
     const int32_t i0 = (lo >> 3) - b0;
     uint32_t v;
     if (i0 >= 0 && i0 + 2 < kBnd) {
-        v = (uint32_t)sDec.bnd[l][i0] | ((uint32_t)sDec.bnd[l][i0 + 1] << 8) | ((uint32_t)sDec.bnd[l][i0 + 2] << 16);
+        v = (uint32_t)bnd_byte(l, i0) | ((uint32_t)bnd_byte(l, i0 + 1) << 8) | ((uint32_t)bnd_byte(l, i0 + 2) << 16);
     } else {
         const int32_t b = lo >> 3;
         v = 0;
@@ -480,12 +483,12 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
 #pragma unroll
         for (int w = 0; w < kBnd / 4; w++) {
             const uint32_t v = ld_word(src, sl, b0 + 4 * w);
-            *(uint32_t*)&sDec.bnd[lane][4 * w] = v;
+            sDec.bnd[w][lane] = v;
         }
     }
     // ---- phase 1: speculative decode of (E, S] into the lane's slice
 #pragma unroll
-    for (int w = 0; w < kBmpBits / 32; w++) sDec.bmp[lane][w] = 0;
+    for (int w = 0; w < kBmpBits / 32; w++) sDec.bmp[w][lane] = 0;
     uint8_t* slice = htmp + (size_t)lane * kSliceCap;
     const uint32_t tmask = (1u << tl) - 1u;
     int32_t q = S;
@@ -500,10 +503,10 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             const int32_t base = round_base(hi);
 #pragma unroll
             for (int i = 0; i < 5; i++) {
-                sDec.stg[lane][4 * i] = nx[i].x;
-                sDec.stg[lane][4 * i + 1] = nx[i].y;
-                sDec.stg[lane][4 * i + 2] = nx[i].z;
-                sDec.stg[lane][4 * i + 3] = nx[i].w;
+                sDec.stg[4 * i][lane] = nx[i].x;
+                sDec.stg[4 * i + 1][lane] = nx[i].y;
+                sDec.stg[4 * i + 2][lane] = nx[i].z;
+                sDec.stg[4 * i + 3][lane] = nx[i].w;
             }
             if (r + 1 < rounds) round_load(nx, src, sl, round_base(hi - kRoundBits));  // next round, in flight
             lds_sync();
@@ -513,14 +516,14 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             int32_t wi = (q - b8 - (int32_t)tl) >> 5;
             wi = wi < 0 ? 0 : (wi > kStgWords - 2 ? kStgWords - 2 : wi);
             int32_t wlo = 32 * wi;
-            uint64_t W = (uint64_t)sDec.stg[lane][wi] | ((uint64_t)sDec.stg[lane][wi + 1] << 32);
-            uint32_t nxw = sDec.stg[lane][wi > 0 ? wi - 1 : 0];
+            uint64_t W = (uint64_t)sDec.stg[wi][lane] | ((uint64_t)sDec.stg[wi + 1][lane] << 32);
+            uint32_t nxw = sDec.stg[wi > 0 ? wi - 1 : 0][lane];
             auto step = [&](bool act) {
                 const int32_t x = q - b8 - (int32_t)tl;
                 const bool rf = x < wlo;
                 W = rf ? ((W << 32) | nxw) : W;
                 wlo = rf ? wlo - 32 : wlo;
-                nxw = sDec.stg[lane][wlo >= 64 ? (wlo >> 5) - 1 : 0];
+                nxw = sDec.stg[wlo >= 64 ? (wlo >> 5) - 1 : 0][lane];
                 const uint32_t e = sDec.tab[(uint32_t)(W >> ((x - wlo) & 63)) & tmask];
                 q = act ? q - (int32_t)(e >> 8) : q;
                 pend |= act ? ((uint64_t)(e & 0xFFu) << (8 * npend)) : 0ull;
@@ -537,7 +540,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             // the first kBmpBits bits below S: record every codeword boundary for the walk
             while (q > lo && S - q < kBmpBits) {
                 const int32_t d = S - q;
-                atomicOr(&sDec.bmp[lane][d >> 5], 1u << (d & 31));
+                atomicOr(&sDec.bmp[d >> 5][lane], 1u << (d & 31));
                 step(true);
                 flush4();
             }
@@ -562,7 +565,8 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     // at l-1's speculative exit, so all 15 walks of a stream run at once; the walk symbols wait in
     // the (now free) staging row.  A stream with a lane that does not meet its boundaries within
     // kBmpBits bits falls back to the serial walker.
-    uint8_t* wsym = (uint8_t*)sDec.stg[lane];
+    // walk symbols: byte t of the lane at word t / 4 of its (now free) staging column
+    auto wsym_at = [&](uint32_t t) -> uint8_t& { return ((uint8_t*)&sDec.stg[t >> 2][lane])[t & 3]; };
     constexpr uint32_t kWalkMax = 4 * kStgWords;
     uint32_t ex = 0;
     int32_t p = (j == 0) ? S : (int32_t)sDec.exitp[lane - 1];
@@ -571,17 +575,17 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         while (p > E && ex < kWalkMax) {
             const int32_t d = S - p;
             if (d >= kBmpBits) break;
-            if ((sDec.bmp[lane][d >> 5] >> (d & 31)) & 1u) { synced = true; break; }
+            if ((sDec.bmp[d >> 5][lane] >> (d & 31)) & 1u) { synced = true; break; }
             const uint32_t e = sDec.tab[walk_peek(lane, S, src, sl, p, tl)];
             p -= (int32_t)(e >> 8);
-            wsym[ex++] = (uint8_t)e;
+            wsym_at(ex++) = (uint8_t)e;
         }
     }
     const int32_t dsync = S - p;
     uint32_t idx = 0;
     if (synced && j > 0) {
-        for (int w = 0; w < (dsync >> 5); w++) idx += (uint32_t)__builtin_popcount(sDec.bmp[lane][w]);
-        if (dsync & 31) idx += (uint32_t)__builtin_popcount(sDec.bmp[lane][dsync >> 5] & ((1u << (dsync & 31)) - 1u));
+        for (int w = 0; w < (dsync >> 5); w++) idx += (uint32_t)__builtin_popcount(sDec.bmp[w][lane]);
+        if (dsync & 31) idx += (uint32_t)__builtin_popcount(sDec.bmp[dsync >> 5][lane] & ((1u << (dsync & 31)) - 1u));
     }
     const uint64_t unsynced = ballot(!synced);
     const bool fast = ((unsynced >> (16 * k)) & 0xFFFFull) == 0;
@@ -622,7 +626,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             while (pp > El) {
                 const int32_t d = Sl - pp;
                 if (d >= kBmpBits) break;  // past the recorded boundaries: finish serially below
-                if ((sDec.bmp[l][d >> 5] >> (d & 31)) & 1u) { sy = true; break; }
+                if ((sDec.bmp[d >> 5][l] >> (d & 31)) & 1u) { sy = true; break; }
                 const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, pp, tl)];
                 pp -= (int32_t)(e >> 8);
                 if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
@@ -631,8 +635,8 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             if (sy) {
                 const int32_t d = Sl - pp;
                 uint32_t ix = 0;
-                for (int w = 0; w < (d >> 5); w++) ix += (uint32_t)__builtin_popcount(sDec.bmp[l][w]);
-                if (d & 31) ix += (uint32_t)__builtin_popcount(sDec.bmp[l][d >> 5] & ((1u << (d & 31)) - 1u));
+                for (int w = 0; w < (d >> 5); w++) ix += (uint32_t)__builtin_popcount(sDec.bmp[w][l]);
+                if (d & 31) ix += (uint32_t)__builtin_popcount(sDec.bmp[d >> 5][l] & ((1u << (d & 31)) - 1u));
                 sDec.skip[l] = ix;
                 sDec.syncd[l] = (uint32_t)d;
                 T = (int32_t)sDec.exitp[l];
@@ -661,7 +665,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     const uint32_t sk = sDec.skip[lane];
     const uint32_t ob = sDec.obase[lane], exl = sDec.extra[lane];
     if (fast)
-        for (uint32_t t = 0; t < exl; t++) gst<uint8_t>(sdst + ob + t, wsym[t]);
+        for (uint32_t t = 0; t < exl; t++) gst<uint8_t>(sdst + ob + t, wsym_at(t));
     const uint32_t o = ob + exl;
     if (c > sk) {
         const uint32_t len = c - sk;
