@@ -544,6 +544,29 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 step(true);
                 flush4();
             }
+            // fast path: every lane still has >= 4 * tl bits in this round, so four symbols decode
+            // unpredicated, with one refill check per pair (2 * tl <= 32 - tl for tl <= 12)
+            const int32_t xb = b8 + (int32_t)tl, tli = (int32_t)tl;
+            while (!ballot(q - lo < 4 * tli)) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const bool rf = (q - xb) - wlo < tli;
+                    W = rf ? ((W << 32) | nxw) : W;
+                    wlo = rf ? wlo - 32 : wlo;
+                    nxw = sDec.stg[wlo >= 64 ? (wlo >> 5) - 1 : 0][lane];
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        const uint32_t e = sDec.tab[(uint32_t)(W >> ((q - xb) - wlo)) & tmask];
+                        q -= (int32_t)(e >> 8);
+                        word |= (e & 0xFFu) << (8 * (2 * h + u));
+                    }
+                }
+                pend |= (uint64_t)word << (8 * npend);
+                if (stored + 4 <= kSliceCap) gst<uint32_t>(slice + stored, (uint32_t)pend);
+                pend >>= 32;
+                stored += 4;
+            }
             while (ballot(q > lo)) {
 #pragma unroll
                 for (int u = 0; u < 4; u++) step(q > lo);
