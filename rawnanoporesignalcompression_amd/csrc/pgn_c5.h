@@ -80,6 +80,53 @@ __device__ __forceinline__ void nwin_flush(uint8_t* W, uint32_t& fill, uint8_t* 
     fill = tail;
 }
 
+// One 1024-sample step (Full: every sample of the step exists).  Per sub-step: three compares give
+// the class ballots (classes combined in scalar registers), each class's bytes go to its window
+// at fill + mbcnt rank under that class's exec mask (class 3 is rare and usually skipped whole),
+// and the quad-OR-ed key byte is written by all four lanes of a quad (same byte, no masking).
+template <bool Full>
+__device__ __forceinline__ void split_step(const int16_t* __restrict__ x, uint32_t n, uint32_t t, SplitLds& W,
+                                           uint32_t& fS, uint32_t& fM, uint32_t& fL, uint32_t& prevX)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t xv[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {  // a partial step re-reads the last sample (masked below)
+        const uint32_t i = t + 64u * (uint32_t)k + lane;
+        xv[k] = (uint32_t)gld<uint16_t>(x + (Full ? i : (i < n ? i : n - 1)));
+    }
+    const uint32_t ksh = 2u * (lane & 3u);
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const uint32_t cur = xv[k];
+        uint32_t prv = dpp<kDppWaveShr1>(cur);
+        prv = (lane == 0) ? prevX : prv;
+        prevX = readlane_u32(cur, 63);
+        const uint32_t v = zz_enc16((uint16_t)(cur - prv));
+        const bool valid = Full || (t + 64u * (uint32_t)k + lane < n);
+        const bool nz = valid && v != 0, gt16 = v > 16, gt272 = v > 272;
+        const uint64_t bnz = ballot(nz), b16 = ballot(gt16), b272 = ballot(gt272);
+        const uint64_t b1 = bnz & ~b16, b2 = bnz & b16 & ~b272, b3 = bnz & b272;
+        if (nz && !gt16) W.S[fS + mbcnt(b1)] = (uint8_t)(v - 1u);
+        if (nz && gt16 && !gt272) W.M[fM + mbcnt(b2)] = (uint8_t)(v - 17u);
+        if (b3) {
+            if (nz && gt272) {
+                const uint32_t w = v - 273u, r = fL + mbcnt(b3);
+                W.L[r] = (uint8_t)w;
+                W.H[r] = (uint8_t)(w >> 8);
+            }
+        }
+        fS += (uint32_t)__builtin_popcountll(b1);
+        fM += (uint32_t)__builtin_popcountll(b2);
+        fL += (uint32_t)__builtin_popcountll(b3);
+        const uint32_t c = (uint32_t)nz + (uint32_t)(nz && gt16) + (uint32_t)(nz && gt272);
+        uint32_t kb = c << ksh;
+        kb |= dpp<kDppQuadSwap1>(kb);
+        kb |= dpp<kDppQuadSwap2>(kb);
+        W.K[16u * (uint32_t)k + (lane >> 2)] = (uint8_t)kb;
+    }
+}
+
 // sizes[5] = {keys, S, M, Llow, Lhigh} bytes.
 __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uint32_t n, const C5Streams& st, uint32_t sizes[5],
                                               SplitLds& W)
@@ -90,39 +137,8 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
     uint32_t prevX = 0;                       // last sample of the previous sub-step (wave-uniform)
     for (uint32_t t = 0; t < n; t += kSplitStep) {
         const bool full = t + kSplitStep <= n;
-        uint32_t xv[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) {  // a partial step re-reads the last sample (masked below)
-            const uint32_t i = t + 64u * (uint32_t)k + lane;
-            xv[k] = (uint32_t)gld<uint16_t>(x + (i < n ? i : n - 1));
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const uint32_t i = t + 64u * (uint32_t)k + lane;
-            const uint32_t cur = xv[k];
-            uint32_t prv = dpp<kDppWaveShr1>(cur);
-            if (lane == 0) prv = prevX;
-            prevX = readlane_u32(cur, 63);
-            const uint32_t v = zz_enc16((uint16_t)(cur - prv));
-            const uint32_t c = (!full && i >= n) ? 0u : (v == 0 ? 0u : (v <= 16 ? 1u : (v <= 272 ? 2u : 3u)));
-            const uint64_t b1 = ballot(c == 1), b2 = ballot(c == 2), b3 = ballot(c == 3);
-            if (c == 1) {
-                W.S[fS + mbcnt(b1)] = (uint8_t)(v - 1u);
-            } else if (c == 2) {
-                W.M[fM + mbcnt(b2)] = (uint8_t)(v - 17u);
-            } else if (c == 3) {
-                const uint32_t w = v - 273u, r = fL + mbcnt(b3);
-                W.L[r] = (uint8_t)w;
-                W.H[r] = (uint8_t)(w >> 8);
-            }
-            fS += (uint32_t)__builtin_popcountll(b1);
-            fM += (uint32_t)__builtin_popcountll(b2);
-            fL += (uint32_t)__builtin_popcountll(b3);
-            uint32_t kb = c << (2u * (lane & 3u));
-            kb |= dpp<kDppQuadSwap1>(kb);
-            kb |= dpp<kDppQuadSwap2>(kb);
-            if ((lane & 3u) == 0) W.K[16u * (uint32_t)k + (lane >> 2)] = (uint8_t)kb;
-        }
+        if (full) split_step<true>(x, n, t, W, fS, fM, fL, prevX);
+        else split_step<false>(x, n, t, W, fS, fM, fL, prevX);
         fH = fL;
         lds_sync();
         const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
