@@ -78,6 +78,65 @@ def cpu_baseline(samples_per_read: int, nreads: int, seed: int):
     }
 
 
+def host_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
+
+
+def stream_copy_gbs(torch, nbytes=4 << 30, reps=5):
+    """Device STREAM-copy ceiling: read + write bytes of a large device-to-device copy."""
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2.0 * nbytes / (ms * 1e-3) / 1e9
+
+
+def pcie_inclusive(torch, codec, S, seed, nreads=2000):
+    """Host-memory rates (pinned buffers, not part of `value`): H2D samples + encode + D2H blobs,
+    and H2D blobs + decode + D2H samples, on a sample of the same workload."""
+    samples, offs, counts = codec.synth_reads(nreads, S, seed=seed)
+    enc = codec.compress_batch(samples, offs, counts)
+    torch.cuda.synchronize()
+    h_samples = samples.cpu().pin_memory()
+    h_blobs = enc.blobs.cpu().pin_memory()
+    h_back = torch.empty_like(h_samples).pin_memory()
+    d_samples = torch.empty_like(samples)
+    d_blobs = torch.empty_like(enc.blobs)
+    out = torch.empty_like(samples)
+    n = nreads * S
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    d_samples.copy_(h_samples, non_blocking=True)
+    e2 = codec.compress_batch(d_samples, offs, counts, out=d_blobs, out_offsets=enc.offsets, out_caps=enc.caps)
+    h_blobs.copy_(d_blobs, non_blocking=True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    d_blobs.copy_(h_blobs, non_blocking=True)
+    codec.decompress_batch(d_blobs, enc.offsets, e2.sizes, counts, out=out, out_offsets=offs)
+    h_back.copy_(out, non_blocking=True)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    return {"encode_msamples_s": round(n / (t1 - t0) / 1e6, 1), "decode_msamples_s": round(n / (t2 - t1) / 1e6, 1),
+            "sample": f"{nreads} reads x {S} samples, pinned host buffers"}
+
+
 def main():
     args = parse()
     import torch
@@ -94,6 +153,10 @@ def main():
 
     codec = PGNanoCodec(local)
     R, S = args.reads, args.samples
+    side = {}
+    if rank == 0 and world == 1:
+        side["stream_copy_gbs"] = round(stream_copy_gbs(torch), 1)
+        side["pcie_inclusive"] = pcie_inclusive(torch, codec, S, args.seed)
     # this rank's shard: global reads rank, rank + world, ... (round-robin)
     sh = shard_reads(R, rank, world)
     samples = torch.empty(R * S, dtype=torch.int16, device="cuda")
@@ -196,8 +259,12 @@ def main():
                 "traffic": traffic,
             },
         }
+        line.update(side)
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(S, args.cpu_sample_reads, args.seed) if world == 1 else None
+            if line["cpu_baseline"]:
+                model, ncpu = host_info()
+                line["cpu_baseline"]["sample"] += f"; host {model}, {ncpu} logical CPUs"
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

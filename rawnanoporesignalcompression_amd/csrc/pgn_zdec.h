@@ -304,21 +304,51 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
         if (nc == 0 || nc >= iSize) return 0;
         lds_sync();
         if (!wdtable_build(sDec.wnorm, maxSV, tl)) return 0;
-        z1::BitR br;
-        if (!z1::br_init(br, sDec.hbuf + 1 + nc, iSize - nc)) return 0;
-        uint32_t st1 = z1::br_read(br, tl), st2 = z1::br_read(br, tl);
+        // FSE weight stream: backward bit container over the staged bytes, the decode table in a
+        // VGPR (entry u in lane u: newState | symbol << 16 | nbBits << 24, read with v_readlane)
+        const uint8_t* bs = sDec.hbuf + 1 + nc;
+        const int32_t bl = (int32_t)(iSize - nc);
+        const uint32_t last = bs[bl - 1];
+        if (last == 0) return 0;
+        int32_t pos = (bl - 1) * 8 + (int32_t)z1::highbit32(last);
+        auto word = [&](int32_t wi) -> uint32_t {  // stream bytes [4wi, 4wi + 4), zero outside
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int32_t i = 4 * wi + b;
+                v |= (i >= 0 && i < bl) ? ((uint32_t)bs[i] << (8 * b)) : 0u;
+            }
+            return v;
+        };
+        int32_t cl = ((pos >> 5) - 1) * 32;  // C holds bits [cl, cl + 64)
+        uint64_t C = (uint64_t)word(cl >> 5) | ((uint64_t)word((cl >> 5) + 1) << 32);
+        auto rd = [&](uint32_t nb) -> uint32_t {
+            const int32_t lo = pos - (int32_t)nb;
+            if (lo < cl) {
+                cl -= 32;
+                C = (C << 32) | word(cl >> 5);
+            }
+            pos = lo;
+            return (uint32_t)(C >> (lo - cl)) & ((1u << nb) - 1u);
+        };
+        const uint32_t tsz = 1u << tl;
+        const uint32_t E = ((uint32_t)lane < tsz)
+                               ? (uint32_t)sDec.wdt[lane].newState | ((uint32_t)sDec.wdt[lane].symbol << 16) |
+                                     ((uint32_t)sDec.wdt[lane].nbBits << 24)
+                               : 0u;
+        uint32_t st1 = rd(tl), st2 = rd(tl);
         // alternate states; stop when the stream overruns (FSE_decompress_usingDTable tail rule)
         while (true) {
             if (nbW > 253) return 0;
-            const z1::FseDEntry e1 = sDec.wdt[st1];
-            sDec.wts[nbW++] = e1.symbol;
-            st1 = e1.newState + z1::br_read(br, e1.nbBits);
-            if (br.pos < 0) { sDec.wts[nbW++] = sDec.wdt[st2].symbol; break; }
+            const uint32_t e1 = readlane_u32(E, (int)st1);
+            sDec.wts[nbW++] = (uint8_t)(e1 >> 16);
+            st1 = (e1 & 0xFFFFu) + rd(e1 >> 24);
+            if (pos < 0) { sDec.wts[nbW++] = (uint8_t)(readlane_u32(E, (int)st2) >> 16); break; }
             if (nbW > 253) return 0;
-            const z1::FseDEntry e2 = sDec.wdt[st2];
-            sDec.wts[nbW++] = e2.symbol;
-            st2 = e2.newState + z1::br_read(br, e2.nbBits);
-            if (br.pos < 0) { sDec.wts[nbW++] = sDec.wdt[st1].symbol; break; }
+            const uint32_t e2 = readlane_u32(E, (int)st2);
+            sDec.wts[nbW++] = (uint8_t)(e2 >> 16);
+            st2 = (e2 & 0xFFFFu) + rd(e2 >> 24);
+            if (pos < 0) { sDec.wts[nbW++] = (uint8_t)(readlane_u32(E, (int)st1) >> 16); break; }
         }
         used = iSize + 1;
     }
@@ -399,14 +429,14 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
         if (sym < nbSym && w4[q]) sDec.order[before[w4[q]] + rankIdx[q]] = (uint8_t)sym;
     }
     lds_sync();
-    const uint32_t tsize = 1u << tl;
-    for (uint32_t u = (uint32_t)lane; u < tsize; u += 64) {
-        unsigned w = 1;
+    // fill weight by weight: weight w owns entries [rankStart[w], rankStart[w] + cntW[w] << (w - 1))
 #pragma unroll
-        for (unsigned ww = 2; ww <= 12; ww++)
-            if (ww <= tl && cntW[ww] && u >= rankStart[ww]) w = ww;
-        const uint32_t k = (u - rankStart[w]) >> (w - 1);
-        sDec.tab[u] = (uint16_t)(sDec.order[before[w] + k] | ((tl + 1 - w) << 8));
+    for (unsigned w = 1; w <= 12; w++) {
+        if (w > tl || cntW[w] == 0) continue;
+        const uint32_t a = rankStart[w], end = a + (cntW[w] << (w - 1));
+        const uint16_t nbb = (uint16_t)((tl + 1 - w) << 8);
+        for (uint32_t u = a + (uint32_t)lane; u < end; u += 64)
+            sDec.tab[u] = (uint16_t)(sDec.order[before[w] + ((u - a) >> (w - 1))] | nbb);
     }
     lds_sync();
     *tlOut = tl;
