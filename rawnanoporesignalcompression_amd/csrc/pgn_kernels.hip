@@ -86,7 +86,7 @@ __host__ __device__ inline DecLayout dec_layout()
     l.lit = take(kMaxStream);
     l.htmp = take((size_t)64 * kSliceCap);
     l.seqs = take(12 * (size_t)kMaxDecSeq);
-    l.tables = take(3 * sizeof(z1::FseDTable));
+    l.tables = take(4 * ((size_t)kSeqTab + 4));
     l.bytes = o;
     return l;
 }
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.htmp = sbase + lay.htmp;
     S.seqs = (uint32_t*)(sbase + lay.seqs);
     S.maxSeq = kMaxDecSeq;
-    S.tables = (z1::FseDTable*)(sbase + lay.tables);
+    S.tables = (uint32_t*)(sbase + lay.tables);
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = kStreams * G;
@@ -544,6 +544,10 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         HIPCHK(hipDeviceSynchronize());
     }
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    // the predefined sequence FSE tables of the decoder (one wave, once per context)
+    hipLaunchKernelGGL(seq_default_tables_kernel, dim3(1), dim3(64), 0, c->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
     *out = c;
     return PGN_OK;
 }

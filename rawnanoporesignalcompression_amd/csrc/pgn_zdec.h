@@ -16,20 +16,35 @@ constexpr uint32_t kSliceCap = 8192;     // speculative symbols kept per lane (h
 constexpr int kBnd = 24;                 // stream bytes [S/8 - 20, S/8 + 4) cached per lane for the walk
 constexpr int kBndBelow = 20;
 
+constexpr int kSeqWin = 2048;            // sequences bitstream window staged in LDS
+constexpr int kSeqHdr = 400;             // staged sequences-section header (table descriptions)
+constexpr int kSeqTab = 1280;            // LL [0,512) + OF [512,768) + ML [768,1280) FSE decode entries
+
 struct DecLds {
     uint16_t tab[1 << z1::kHufTableLogMax];  // Huffman decode table: symbol | nbBits << 8
-    // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
-    uint32_t bmp[kBmpBits / 32][64];         // speculative decode: boundary bitmap below each lane start
-    uint32_t stg[kStgWords][64];             // staged stream bytes of the current round
-    uint32_t bnd[kBnd / 4][64];              // bytes around each lane's start (phase-2 walk), word-major
-    uint32_t cnt[64], startp[64], endp[64], exitp[64], skip[64], extra[64], obase[64], syncd[64];
-    uint8_t wts[256];                        // weights of the current table
-    uint8_t order[256];                      // symbols sorted by (weight, symbol)
-    uint8_t hbuf[272];                       // staged Huffman table description (zero padded)
-    z1::FseDEntry wdt[64];                   // weights FSE decode table (tableLog <= 6)
-    int16_t wnorm[16];
-    uint16_t wnext[16];
-    uint32_t wrank[16];
+    union {
+        struct {  // literals stage
+            // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
+            uint32_t bmp[kBmpBits / 32][64];  // speculative decode: boundary bitmap below each lane start
+            uint32_t stg[kStgWords][64];      // staged stream bytes of the current round
+            uint32_t bnd[kBnd / 4][64];       // bytes around each lane's start (phase-2 walk)
+            uint32_t cnt[64], startp[64], endp[64], exitp[64], skip[64], extra[64], obase[64], syncd[64];
+            uint8_t wts[256];                 // weights of the current table
+            uint8_t order[256];               // symbols sorted by (weight, symbol)
+            uint8_t hbuf[272];                // staged Huffman table description (zero padded)
+            z1::FseDEntry wdt[64];            // weights FSE decode table (tableLog <= 6)
+            int16_t wnorm[16];
+            uint16_t wnext[16];
+            uint32_t wrank[16];
+        };
+        struct {  // sequences stage
+            uint32_t qtab[kSeqTab];           // FSE entries: newState | symbol << 16 | nbBits << 24
+            int16_t qnorm[64];
+            uint32_t qsq[64][3];              // a batch of decoded sequences: litLength, matchLength, offset
+            uint8_t qhdr[kSeqHdr];
+            uint8_t qwin[kSeqWin];
+        };
+    };
     uint32_t u[16];
 };
 
@@ -41,7 +56,7 @@ struct DecScratch {
     uint8_t* htmp;          // 64 * kSliceCap speculative Huffman symbols
     uint32_t* seqs;         // decoded sequences: {litLength, matchLength, offset} triples
     uint32_t maxSeq;
-    z1::FseDTable* tables;  // ll, of, ml
+    uint32_t* tables;       // the three sequence FSE tables of a multi-block frame (kSeqTab + 4 words)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -761,84 +776,128 @@ __device__ __noinline__ bool huf_decode1_lane(unsigned tl, const uint8_t* src, s
     return pos == 0;
 }
 
-// Decode the sequences section into a list (lane 0).  Returns nbSeq or -1.
-__device__ __noinline__ long decode_seq_list(const uint8_t* src, size_t srcSize, const DecScratch& S, uint32_t rep[3],
-                                       bool valid[3])
+// ---------------------------------------------------------------------------------------------
+// Sequences (ZSTD_decodeSeqHeaders + ZSTD_decodeSequence + execution), wave-uniform.  The three FSE
+// decode tables are built in LDS (the predefined ones are copied from gSeqDefTab); the bitstream
+// is read backwards through a window staged into LDS; sequences are decoded 64 at a time into LDS
+// and executed by the whole wave.  Frame state lives in sDec.u: [2..4] repeat offsets, [5] bit k =
+// table k valid (repeat mode), [6] bit k = table k saved to S.tables (multi-block frames).
+// ---------------------------------------------------------------------------------------------
+__device__ uint32_t gSeqDefTab[kSeqTab + 4];  // predefined LL / OF / ML tables (+ their logs), filled once
+
+__device__ __forceinline__ uint32_t seq_tab_off(int k) { return k == 0 ? 0u : (k == 1 ? 512u : 768u); }
+
+// FSE_buildDTable into sDec.qtab + off, wave-uniform; symbolNext lives in a VGPR (lane s).
+__device__ __forceinline__ bool qtable_build(uint32_t off, unsigned maxSV, unsigned tableLog)
 {
-    size_t nbSeq = gb(src + (0));
-    size_t pos = 1;
-    if (nbSeq >= 128) {
-        if (nbSeq == 255) {
-            if (srcSize < 3) return -1;
-            nbSeq = (size_t)(gb(src + (1)) | (gb(src + (2)) << 8)) + 0x7F00;
-            pos = 3;
-        } else {
-            if (srcSize < 2) return -1;
-            nbSeq = ((nbSeq - 128) << 8) + gb(src + (1));
-            pos = 2;
+    const int lane = lane_id();
+    const int16_t* norm = sDec.qnorm;
+    const uint32_t tableSize = 1u << tableLog;
+    const uint32_t mask = tableSize - 1;
+    const uint32_t step = (tableSize >> 1) + (tableSize >> 3) + 3;
+    uint32_t highThreshold = tableSize - 1;
+    uint32_t nextV = 0;
+    for (unsigned sy = 0; sy <= maxSV; sy++) {
+        const int nv = norm[sy];
+        if (nv == -1) sDec.qtab[off + highThreshold--] = sy << 16;
+        nextV = (lane == (int)sy) ? (uint32_t)(nv == -1 ? 1 : nv) : nextV;
+    }
+    uint32_t position = 0;
+    for (unsigned sy = 0; sy <= maxSV; sy++) {
+        const int nv = norm[sy];
+        for (int i = 0; i < nv; i++) {
+            sDec.qtab[off + position] = sy << 16;
+            position = (position + step) & mask;
+            while (position > highThreshold) position = (position + step) & mask;
         }
     }
-    if (nbSeq == 0) return (pos == srcSize) ? 0 : -1;
-    if (nbSeq > S.maxSeq || pos >= srcSize) return -1;
-    const uint8_t modes = gb(src + (pos++));
-    z1::FseDTable& ll = S.tables[0];
-    z1::FseDTable& of = S.tables[1];
-    z1::FseDTable& ml = S.tables[2];
-    size_t r = z1::build_seq_dtable(ll, valid[0], modes >> 6, src + pos, srcSize - pos, 0);
-    if (r == (size_t)-1) return -1;
-    pos += r;
-    r = z1::build_seq_dtable(of, valid[1], (modes >> 4) & 3, src + pos, srcSize - pos, 1);
-    if (r == (size_t)-1) return -1;
-    pos += r;
-    r = z1::build_seq_dtable(ml, valid[2], (modes >> 2) & 3, src + pos, srcSize - pos, 2);
-    if (r == (size_t)-1) return -1;
-    pos += r;
-    z1::BitR br;
-    if (!z1::br_init(br, src + pos, srcSize - pos)) return -1;
-    uint32_t sLL = z1::br_read(br, ll.tableLog);
-    uint32_t sOF = z1::br_read(br, of.tableLog);
-    uint32_t sML = z1::br_read(br, ml.tableLog);
-    for (size_t i = 0; i < nbSeq; i++) {
-        const z1::FseDEntry eLL = ll.e[sLL], eOF = of.e[sOF], eML = ml.e[sML];
-        const unsigned ofCode = eOF.symbol, mlCode = eML.symbol, llCode = eLL.symbol;
-        if (ofCode > 31) return -1;
-        const uint32_t ofv = z1::of_value(ofCode, br);
-        const uint32_t mlen = z1::ml_base(mlCode) + z1::br_read(br, z1::ml_bits(mlCode));
-        const uint32_t llen = z1::ll_base(llCode) + z1::br_read(br, z1::ll_bits(llCode));
-        uint32_t offset;
-        if (ofv > 3) {
-            offset = ofv - 3;
-            rep[2] = rep[1]; rep[1] = rep[0]; rep[0] = offset;
-        } else {
-            unsigned idx = ofv - 1 + (llen == 0 ? 1u : 0u);
-            if (idx == 0) {
-                offset = rep[0];
-            } else {
-                offset = (idx == 3) ? rep[0] - 1 : rep[idx];
-                if (offset == 0) offset = 1;
-                if (idx != 1) rep[2] = rep[1];
-                rep[1] = rep[0];
-                rep[0] = offset;
-            }
-        }
-        if (i + 1 < nbSeq) {
-            sLL = eLL.newState + z1::br_read(br, eLL.nbBits);
-            sML = eML.newState + z1::br_read(br, eML.nbBits);
-            sOF = eOF.newState + z1::br_read(br, eOF.nbBits);
-        }
-        S.seqs[3 * i] = llen;
-        S.seqs[3 * i + 1] = mlen;
-        S.seqs[3 * i + 2] = offset;
+    if (position != 0) return false;
+    lds_sync();
+    for (uint32_t u = 0; u < tableSize; u++) {
+        const uint32_t sy = (sDec.qtab[off + u] >> 16) & 0xFFu;
+        const uint32_t nextState = readlane_u32(nextV, (int)sy);
+        nextV = (lane == (int)sy) ? nextState + 1 : nextV;
+        const uint32_t nb = tableLog - z1::highbit32(nextState);
+        sDec.qtab[off + u] = ((nextState << nb) - tableSize) | (sy << 16) | (nb << 24);
     }
-    if (br.pos != 0) return -1;
-    return (long)nbSeq;
+    lds_sync();
+    return true;
 }
 
-// Sequences of one block: the list on lane 0, execution (literal + match copies) on the wave.
-// Returns the new output position or a negative z1::DecErr.
+// one-time build of the predefined tables (launched once per context, one wave)
+__global__ __launch_bounds__(64) void seq_default_tables_kernel()
+{
+    const int lane = lane_id();
+#pragma unroll 1
+    for (int k = 0; k < 3; k++) {
+        const unsigned dmax = k == 0 ? z1::kMaxLL : (k == 1 ? z1::kDefaultMaxOff : z1::kMaxML);
+        const unsigned lg = k == 0 ? z1::kLLDefaultNormLog : (k == 1 ? z1::kOFDefaultNormLog : z1::kMLDefaultNormLog);
+        if ((unsigned)lane <= dmax)
+            sDec.qnorm[lane] = k == 0 ? z1::ll_default_norm(lane) : (k == 1 ? z1::of_default_norm(lane) : z1::ml_default_norm(lane));
+        lds_sync();
+        qtable_build(seq_tab_off(k), dmax, lg);
+        for (uint32_t u = (uint32_t)lane; u < (1u << lg); u += 64) gSeqDefTab[seq_tab_off(k) + u] = sDec.qtab[seq_tab_off(k) + u];
+        if (lane == 0) gSeqDefTab[kSeqTab + k] = lg;
+        lds_sync();
+    }
+}
+
+// backward bit reader over the sequences bitstream [0, len) of `bs` (global), through an LDS window
+struct SeqBits {
+    const uint8_t* bs;
+    int32_t len;
+    int32_t pos;   // unread bits
+    int32_t wb;    // first stream byte held in sDec.qwin
+    uint64_t C;    // stream bits [cl, cl + 64)
+    int32_t cl;
+};
+__device__ __forceinline__ void seqbits_stage(SeqBits& b, int32_t needByte)
+{
+    // window [wb, wb + kSeqWin) ending just above the byte needed (or the stream end)
+    int32_t top = needByte + 16 < b.len ? needByte + 16 : b.len;
+    int32_t wb = top - kSeqWin;
+    wb = wb < 0 ? 0 : wb;
+    const int lane = lane_id();
+    for (int32_t i = lane * 16; i < kSeqWin; i += 64 * 16) {
+        const int32_t g = wb + i;
+        if (g + 16 <= b.len) {
+            *(uint4*)(sDec.qwin + i) = gld<uint4>(b.bs + g);
+        } else {
+            for (int t = 0; t < 16; t++) sDec.qwin[i + t] = (g + t < b.len) ? gb(b.bs + g + t) : (uint8_t)0;
+        }
+    }
+    b.wb = wb;
+    lds_sync();
+}
+__device__ __forceinline__ uint32_t seqbits_word(SeqBits& b, int32_t wi)  // stream bytes [4wi, 4wi + 4)
+{
+    const int32_t g = 4 * wi;
+    if (g + 4 <= 0 || g >= b.len) return 0u;
+    if (g < b.wb || g + 4 > b.wb + kSeqWin) seqbits_stage(b, g + 3 > 0 ? g + 3 : 0);
+    uint32_t v = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int32_t i = g + t;
+        v |= (i >= 0 && i < b.len) ? ((uint32_t)sDec.qwin[i - b.wb] << (8 * t)) : 0u;
+    }
+    return v;
+}
+__device__ __forceinline__ uint32_t seqbits_read(SeqBits& b, uint32_t nb)
+{
+    if (nb == 0) return 0;
+    const int32_t lo = b.pos - (int32_t)nb;
+    if (lo < b.cl) {
+        b.cl -= 32;
+        b.C = (b.C << 32) | seqbits_word(b, b.cl >> 5);
+    }
+    b.pos = lo;
+    return (uint32_t)(b.C >> (lo - b.cl)) & (uint32_t)((1ull << nb) - 1ull);
+}
+
+// One block's sequences: decode + execute.  Returns the new output position or a negative DecErr.
 __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t seqSize, const uint8_t* lit, size_t rs,
                                                  uint8_t* dst, size_t op, size_t dstCap, size_t frameStart,
-                                                 DecScratch S, uint32_t rep[3], bool tvalid[3])
+                                                 DecScratch S, bool lastBlock)
 {
     const int lane = lane_id();
     seqSrc = uni(seqSrc);
@@ -849,41 +908,178 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
     op = uni((uint64_t)op);
     dstCap = uni((uint64_t)dstCap);
     frameStart = uni((uint64_t)frameStart);
-    S.lit = uni(S.lit);
-    S.htmp = uni(S.htmp);
     S.seqs = uni(S.seqs);
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
-    if (lane == 0) {
-        long nb = decode_seq_list(seqSrc, seqSize, S, rep, tvalid);
-        sDec.u[1] = (uint32_t)(nb < 0 ? 0xFFFFFFFFu : (uint32_t)nb);
-        sDec.u[2] = rep[0]; sDec.u[3] = rep[1]; sDec.u[4] = rep[2];
-        sDec.u[5] = tvalid[0]; sDec.u[6] = tvalid[1]; sDec.u[7] = tvalid[2];
+    // stage the section head (nbSeq, modes, table descriptions), zero padded
+    const uint32_t nst = seqSize < (size_t)kSeqHdr - 16 ? (uint32_t)seqSize : (uint32_t)kSeqHdr - 16;
+    for (uint32_t i = (uint32_t)lane; i < (uint32_t)kSeqHdr; i += 64) sDec.qhdr[i] = i < nst ? gb(seqSrc + i) : (uint8_t)0;
+    lds_sync();
+    const int32_t srcSize = (int32_t)seqSize;
+    uint32_t nbSeq = sDec.qhdr[0];
+    int32_t pos = 1;
+    if (nbSeq >= 128) {
+        if (nbSeq == 255) {
+            if (srcSize < 3) return z1::kDecErrCorrupt;
+            nbSeq = ((uint32_t)sDec.qhdr[1] | ((uint32_t)sDec.qhdr[2] << 8)) + 0x7F00;
+            pos = 3;
+        } else {
+            if (srcSize < 2) return z1::kDecErrCorrupt;
+            nbSeq = ((nbSeq - 128) << 8) + sDec.qhdr[1];
+            pos = 2;
+        }
     }
-    wave_sync();
-    const uint32_t nb = sDec.u[1];
-    if (nb == 0xFFFFFFFFu) return z1::kDecErrCorrupt;
-    rep[0] = sDec.u[2]; rep[1] = sDec.u[3]; rep[2] = sDec.u[4];
-    tvalid[0] = sDec.u[5]; tvalid[1] = sDec.u[6]; tvalid[2] = sDec.u[7];
-    size_t litPos = 0;
-    for (uint32_t i = 0; i < nb; i++) {
-        const uint32_t ll = S.seqs[3 * i], ml = S.seqs[3 * i + 1], off = S.seqs[3 * i + 2];
-        if (litPos + ll > rs) return z1::kDecErrCorrupt;
-        if (op + ll + ml > dstCap) return z1::kDecErrDstSmall;
-        wave_copy(dst + op, lit + litPos, ll);
-        litPos += ll;
-        op += ll;
-        if ((size_t)off > op - frameStart) return z1::kDecErrCorrupt;
-        wave_sync();
-        for (uint32_t k = (uint32_t)lane; k < ml; k += 64) gst<uint8_t>(dst + op + k, gb(dst + op - off + (k % off)));
-        op += ml;
-        wave_sync();
+    uint32_t rep0 = sDec.u[2], rep1 = sDec.u[3], rep2 = sDec.u[4];
+    uint32_t valid = sDec.u[5];
+    if (nbSeq == 0) {
+        if (pos != srcSize) return z1::kDecErrCorrupt;
+    } else {
+        if (nbSeq > S.maxSeq || pos >= srcSize) return z1::kDecErrCorrupt;
+        const uint32_t modes = sDec.qhdr[pos++];
+        uint32_t tlog[3];
+#pragma unroll 1
+        for (int k = 0; k < 3; k++) {
+            const unsigned mode = (modes >> (6 - 2 * k)) & 3u;
+            const uint32_t off = seq_tab_off(k);
+            const unsigned maxS = k == 0 ? z1::kMaxLL : (k == 1 ? z1::kMaxOff : z1::kMaxML);
+            const unsigned maxLog = k == 0 ? z1::kLLFSELog : (k == 1 ? z1::kOffFSELog : z1::kMLFSELog);
+            if (mode == z1::kSetBasic) {
+                const uint32_t lg = gSeqDefTab[kSeqTab + k];
+                for (uint32_t u = (uint32_t)lane; u < (1u << lg); u += 64) sDec.qtab[off + u] = gSeqDefTab[off + u];
+                tlog[k] = lg;
+            } else if (mode == z1::kSetRle) {
+                if (pos >= srcSize || sDec.qhdr[pos] > maxS) return z1::kDecErrCorrupt;
+                if (lane == 0) sDec.qtab[off] = (uint32_t)sDec.qhdr[pos] << 16;
+                tlog[k] = 0;
+                pos += 1;
+            } else if (mode == z1::kSetCompressed) {
+                if (pos >= kSeqHdr - 16) return z1::kDecErrCorrupt;  // description beyond the staged head
+                unsigned maxSV = maxS, tl = 0;
+                const int32_t avail = srcSize - pos;
+                const size_t nc = ncount_lds(sDec.qnorm, &maxSV, &tl, sDec.qhdr + pos, (size_t)avail,
+                                             avail < 8 ? 8 : (size_t)avail, maxLog);
+                if (nc == 0) return z1::kDecErrCorrupt;
+                lds_sync();
+                if (!qtable_build(off, maxSV, tl)) return z1::kDecErrCorrupt;
+                tlog[k] = tl;
+                pos += (int32_t)nc;
+            } else {  // repeat: the previous block's table (saved to HBM)
+                if (!((valid >> k) & 1u) || !((sDec.u[6] >> k) & 1u)) return z1::kDecErrCorrupt;
+                const uint32_t lg = S.tables[kSeqTab + k];
+                for (uint32_t u = (uint32_t)lane; u < (1u << lg); u += 64) sDec.qtab[off + u] = S.tables[off + u];
+                tlog[k] = lg;
+            }
+            valid |= 1u << k;
+            lds_sync();
+        }
+        if (!lastBlock) {  // a later block may repeat these tables
+            for (int k = 0; k < 3; k++) {
+                const uint32_t off = seq_tab_off(k);
+                for (uint32_t u = (uint32_t)lane; u < (1u << tlog[k]); u += 64) gst<uint32_t>(S.tables + off + u, sDec.qtab[off + u]);
+                if (lane == 0) gst<uint32_t>(S.tables + kSeqTab + k, tlog[k]);
+            }
+            if (lane == 0) sDec.u[6] = 7u;
+        }
+        // bitstream
+        SeqBits br;
+        br.bs = seqSrc + pos;
+        br.len = srcSize - pos;
+        if (br.len <= 0) return z1::kDecErrCorrupt;
+        const uint8_t lastB = gb(br.bs + br.len - 1);
+        if (lastB == 0) return z1::kDecErrCorrupt;
+        br.pos = (br.len - 1) * 8 + (int32_t)z1::highbit32(lastB);
+        seqbits_stage(br, br.len - 1);
+        br.cl = ((br.pos >> 5) - 1) * 32;
+        br.C = (uint64_t)seqbits_word(br, br.cl >> 5) | ((uint64_t)seqbits_word(br, (br.cl >> 5) + 1) << 32);
+        uint32_t sLL = seqbits_read(br, tlog[0]);
+        uint32_t sOF = seqbits_read(br, tlog[1]);
+        uint32_t sML = seqbits_read(br, tlog[2]);
+        size_t litPos = 0;
+        for (uint32_t b0 = 0; b0 < nbSeq; b0 += 64) {
+            const uint32_t nb = (nbSeq - b0) < 64u ? nbSeq - b0 : 64u;
+            // decode a batch
+            for (uint32_t t = 0; t < nb; t++) {
+                const uint32_t eLL = sDec.qtab[sLL], eOF = sDec.qtab[512 + sOF], eML = sDec.qtab[768 + sML];
+                const uint32_t ofCode = (eOF >> 16) & 0xFFu, mlCode = (eML >> 16) & 0xFFu, llCode = (eLL >> 16) & 0xFFu;
+                if (ofCode > 31) return z1::kDecErrCorrupt;
+                const uint32_t ofv = (1u << ofCode) + seqbits_read(br, ofCode);
+                const uint32_t mlen = z1::ml_base(mlCode) + seqbits_read(br, z1::ml_bits(mlCode));
+                const uint32_t llen = z1::ll_base(llCode) + seqbits_read(br, z1::ll_bits(llCode));
+                uint32_t offset;
+                if (ofv > 3) {
+                    offset = ofv - 3;
+                    rep2 = rep1;
+                    rep1 = rep0;
+                    rep0 = offset;
+                } else {
+                    const unsigned idx = ofv - 1 + (llen == 0 ? 1u : 0u);
+                    if (idx == 0) {
+                        offset = rep0;
+                    } else {
+                        offset = (idx == 3) ? rep0 - 1 : (idx == 1 ? rep1 : rep2);
+                        if (offset == 0) offset = 1;
+                        if (idx != 1) rep2 = rep1;
+                        rep1 = rep0;
+                        rep0 = offset;
+                    }
+                }
+                if (b0 + t + 1 < nbSeq) {
+                    sLL = (eLL & 0xFFFFu) + seqbits_read(br, eLL >> 24);
+                    sML = (eML & 0xFFFFu) + seqbits_read(br, eML >> 24);
+                    sOF = (eOF & 0xFFFFu) + seqbits_read(br, eOF >> 24);
+                }
+                if (lane == 0) {
+                    sDec.qsq[t][0] = llen;
+                    sDec.qsq[t][1] = mlen;
+                    sDec.qsq[t][2] = offset;
+                }
+            }
+            lds_sync();
+            // execute the batch
+            for (uint32_t t = 0; t < nb; t++) {
+                const uint32_t ll = sDec.qsq[t][0], ml = sDec.qsq[t][1], off = sDec.qsq[t][2];
+                if (litPos + ll > rs) return z1::kDecErrCorrupt;
+                if (op + ll + ml > dstCap) return z1::kDecErrDstSmall;
+                wave_copy(dst + op, lit + litPos, ll);
+                litPos += ll;
+                op += ll;
+                if ((size_t)off > op - frameStart) return z1::kDecErrCorrupt;
+                lds_sync();
+                if (off >= 64 || off >= ml) {  // no overlap within a 64-byte step
+                    for (uint32_t k = (uint32_t)lane; k < ml; k += 64) gst<uint8_t>(dst + op + k, gb(dst + op - off + k));
+                } else {  // repeating pattern of period off: byte k = pattern[k mod off]
+                    uint32_t r = (uint32_t)lane % off;
+                    const uint32_t adv = 64u % off;
+                    for (uint32_t k = (uint32_t)lane; k < ml; k += 64) {
+                        gst<uint8_t>(dst + op + k, gb(dst + op - off + r));
+                        r += adv;
+                        r = r >= off ? r - off : r;
+                    }
+                }
+                op += ml;
+                lds_sync();
+            }
+        }
+        if (br.pos != 0) return z1::kDecErrCorrupt;
+        const size_t remLit = rs - litPos;
+        if (op + remLit > dstCap) return z1::kDecErrDstSmall;
+        wave_copy(dst + op, lit + litPos, remLit);
+        op += remLit;
+        lds_sync();
+        if (lane == 0) {
+            sDec.u[2] = rep0;
+            sDec.u[3] = rep1;
+            sDec.u[4] = rep2;
+            sDec.u[5] = valid;
+        }
+        lds_sync();
+        return (long)op;
     }
-    const size_t remLit = rs - litPos;
-    if (op + remLit > dstCap) return z1::kDecErrDstSmall;
-    wave_copy(dst + op, lit + litPos, remLit);
-    op += remLit;
-    wave_sync();
+    // no sequences: the literals are the block
+    if (op + rs > dstCap) return z1::kDecErrDstSmall;
+    wave_copy(dst + op, lit, rs);
+    op += rs;
+    lds_sync();
     return (long)op;
 }
 
@@ -937,8 +1133,14 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
         const size_t frameStart = op;
         bool hufValid = false;
         unsigned hufTl = 0;
-        bool tvalid[3] = {false, false, false};
-        uint32_t rep[3] = {1, 4, 8};
+        if (lane == 0) {  // frame state of the sequences stage: repeat offsets, table validity
+            sDec.u[2] = 1;
+            sDec.u[3] = 4;
+            sDec.u[4] = 8;
+            sDec.u[5] = 0;
+            sDec.u[6] = 0;
+        }
+        lds_sync();
         while (true) {
             if (srcSize - ip < 3) return z1::kDecErrSrcSmall;
             const uint32_t bh = (uint32_t)gb(src + (ip)) | ((uint32_t)gb(src + (ip + 1)) << 8) | ((uint32_t)gb(src + (ip + 2)) << 16);
@@ -1025,7 +1227,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                 if (noSeq) {
                     op += rs;
                 } else {
-                    const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, rep, tvalid);
+                    const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, last != 0);
                     if (r < 0) return r;
                     op = (size_t)r;
                     P.mark(4);

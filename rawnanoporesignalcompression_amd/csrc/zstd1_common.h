@@ -38,46 +38,46 @@ enum : unsigned { kBtRaw = 0, kBtRle = 1, kBtCompressed = 2 };
 // ---------------------------------------------------------------------------------------------
 PGN_HD unsigned ll_bits(unsigned code)
 {
-    constexpr uint8_t t[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  1,  1,
+    static constexpr uint8_t t[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  1,  1,
                                1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
     return t[code];
 }
 PGN_HD unsigned ml_bits(unsigned code)
 {
-    constexpr uint8_t t[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+    static constexpr uint8_t t[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1,
                                2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
     return t[code];
 }
 PGN_HD int16_t ll_default_norm(unsigned s)
 {
-    constexpr int16_t t[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+    static constexpr int16_t t[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
                                2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
     return t[s];
 }
 PGN_HD int16_t ml_default_norm(unsigned s)
 {
-    constexpr int16_t t[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+    static constexpr int16_t t[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
                                1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
     return t[s];
 }
 PGN_HD int16_t of_default_norm(unsigned s)
 {
-    constexpr int16_t t[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+    static constexpr int16_t t[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                                1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
     return t[s];
 }
 PGN_HD uint32_t ll_base(unsigned code)
 {
-    constexpr uint32_t t[36] = {0,  1,  2,  3,  4,  5,   6,   7,   8,    9,    10,   11,
+    static constexpr uint32_t t[36] = {0,  1,  2,  3,  4,  5,   6,   7,   8,    9,    10,   11,
                                 12, 13, 14, 15, 16, 18,  20,  22,  24,   28,   32,   40,
                                 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
     return t[code];
 }
 PGN_HD uint32_t ml_base(unsigned code)  // match length (not mlBase): 3 + ...
 {
-    constexpr uint32_t t[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16,
+    static constexpr uint32_t t[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16,
                                 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30,
                                 31, 32, 33, 34, 35, 37, 39, 41, 43, 47, 51, 59, 67, 83,
                                 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
@@ -88,7 +88,7 @@ PGN_HD unsigned highbit32(uint32_t v) { return 31u - (unsigned)__builtin_clz(v);
 
 PGN_HD unsigned ll_code(uint32_t litLength)
 {
-    constexpr uint8_t t[64] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+    static constexpr uint8_t t[64] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
                                16, 16, 17, 17, 18, 18, 19, 19, 20, 20, 20, 20, 21, 21, 21, 21,
                                22, 22, 22, 22, 22, 22, 22, 22, 23, 23, 23, 23, 23, 23, 23, 23,
                                24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24};
