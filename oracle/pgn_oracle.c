@@ -101,6 +101,37 @@ size_t pgno_zstd_compress1(const uint8_t *src, size_t n, uint8_t *dst, size_t ca
     return Z.iserror(r) ? (size_t)-1 : r;
 }
 
+/* Frames from other encoder settings, for decoder coverage only (the reference itself always
+ * writes level 1).  window_log == 0: ZSTD_compress at `level`.  window_log > 0: the advanced API
+ * with ZSTD_c_windowLog forced, which splits the input into blocks of 1 << window_log bytes
+ * (multi-block frames: repeat-mode tables, offsets reaching into earlier blocks) and writes a
+ * window descriptor instead of a single-segment header. */
+typedef void *(*fn_cctx_new)(void);
+typedef size_t (*fn_cctx_free)(void *);
+typedef size_t (*fn_cctx_set)(void *, int, int);
+typedef size_t (*fn_compress2)(void *, void *, size_t, const void *, size_t);
+size_t pgno_zstd_compress_ex(const uint8_t *src, size_t n, uint8_t *dst, size_t cap, int level, int window_log)
+{
+    if (!zok()) return (size_t)-1;
+    if (window_log == 0) {
+        size_t r = Z.compress(dst, cap, src, n, level);
+        return Z.iserror(r) ? (size_t)-1 : r;
+    }
+    fn_cctx_new cnew = (fn_cctx_new)dlsym(Z.h, "ZSTD_createCCtx");
+    fn_cctx_free cfree = (fn_cctx_free)dlsym(Z.h, "ZSTD_freeCCtx");
+    fn_cctx_set cset = (fn_cctx_set)dlsym(Z.h, "ZSTD_CCtx_setParameter");
+    fn_compress2 c2 = (fn_compress2)dlsym(Z.h, "ZSTD_compress2");
+    if (!cnew || !cfree || !cset || !c2) return (size_t)-1;
+    void *cc = cnew();
+    if (!cc) return (size_t)-1;
+    size_t r = cset(cc, 100 /* ZSTD_c_compressionLevel */, level);
+    if (!Z.iserror(r)) r = cset(cc, 101 /* ZSTD_c_windowLog */, window_log);
+    if (!Z.iserror(r)) r = cset(cc, 200 /* ZSTD_c_contentSizeFlag */, 1);
+    if (!Z.iserror(r)) r = c2(cc, dst, cap, src, n);
+    cfree(cc);
+    return Z.iserror(r) ? (size_t)-1 : r;
+}
+
 size_t pgno_zstd_decompress(const uint8_t *src, size_t n, uint8_t *dst, size_t cap)
 {
     if (!zok()) return (size_t)-1;

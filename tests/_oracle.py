@@ -30,6 +30,8 @@ def oracle() -> C.CDLL:
         L.pgno_zstd_bound.argtypes = [C.c_size_t]
         L.pgno_zstd_compress1.restype = C.c_size_t
         L.pgno_zstd_compress1.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
+        L.pgno_zstd_compress_ex.restype = C.c_size_t
+        L.pgno_zstd_compress_ex.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int, C.c_int]
         L.pgno_zstd_decompress.restype = C.c_size_t
         L.pgno_zstd_decompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]
         L.pgno_c5_bound.restype = C.c_size_t
@@ -77,6 +79,39 @@ def zstd_compress1(data: bytes | np.ndarray) -> bytes:
     r = L.pgno_zstd_compress1(a.ctypes.data if a.size else 0, a.size, out.ctypes.data, cap)
     assert r != (1 << 64) - 1
     return out[:r].tobytes()
+
+
+def zstd_compress_ex(data, level: int, window_log: int = 0) -> bytes:
+    """libzstd frame at another level / forced window (decoder coverage; the reference writes level 1)."""
+    L = oracle()
+    a = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data,
+                             dtype=np.uint8)
+    cap = L.pgno_zstd_bound(a.size) + 64
+    out = np.zeros(cap + 16, np.uint8)
+    r = L.pgno_zstd_compress_ex(a.ctypes.data if a.size else 0, a.size, out.ctypes.data, cap, level, window_log)
+    assert r != (1 << 64) - 1
+    return out[:r].tobytes()
+
+
+def c5_streams(x: np.ndarray) -> list[bytes]:
+    """The five raw C5 streams [keys, S, M, Llow, Lhigh] of one chunk (C5.hpp:282-415)."""
+    L = oracle()
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    n = x.size
+    bufs = [np.zeros((n + 3) // 4 + 1, np.uint8)] + [np.zeros(n + 1, np.uint8) for _ in range(4)]
+    sz = np.zeros(5, np.uint64)
+    L.pgno_c5_split(x.ctypes.data if n else 0, n, *[b.ctypes.data for b in bufs], sz.ctypes.data)
+    return [bufs[i][: int(sz[i])].tobytes() for i in range(5)]
+
+
+def c5_assemble(frames: list[bytes]) -> bytes:
+    """C5 wire format from five zstd frames: [u64 cK][K][u64 cS][S][u64 cM][M][u64 cLl][Ll][Lh]."""
+    out = b""
+    for s, f in enumerate(frames):
+        if s < 4:
+            out += len(f).to_bytes(8, "little")
+        out += f
+    return out
 
 
 def c5_compress(x: np.ndarray, cap: int | None = None):

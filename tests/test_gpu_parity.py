@@ -166,3 +166,33 @@ def test_full_size_chunks_round_trip(codec):
         assert blobs[bo[r]:bo[r] + bs[r]].tobytes() == ref, r
     bits = 8.0 * float(enc.sizes.sum().item()) / (n * k)
     assert 5.0 < bits < 8.0
+
+
+def test_decode_frames_from_other_encoder_settings(codec):
+    """The reference decodes whatever libzstd frames a blob holds (ZSTD_decompress, C5.hpp:520-600).
+    Blobs whose five frames come from other levels (compressed FSE sequence tables, 1-stream
+    literals, long matches) or forced small windows (multi-block frames, repeat-mode tables,
+    window-descriptor headers) decode to the original samples -- one at a time and batched."""
+    import torch
+
+    settings = [(3, 0), (9, 0), (19, 0), (-5, 0), (1, 10), (6, 12), (19, 11), (22, 17)]
+    sigs = [O.synth_read(900 + i, n) for i, n in enumerate([5, 300, 4099, 20000, 65792, 102400, 131072])]
+    sigs += list(_pattern_signals().values())
+    blobs, want = [], []
+    for level, wlog in settings:
+        for x in sigs:
+            blob = O.c5_assemble([O.zstd_compress_ex(s, level, wlog) for s in O.c5_streams(x)])
+            got = codec.decompress_signal(blob, sample_count=x.size)
+            assert np.array_equal(got, x), (level, wlog, x.size)
+            blobs.append(blob)
+            want.append(x)
+    sizes = np.array([len(b) for b in blobs], np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    flat = np.frombuffer(b"".join(blobs), np.uint8)
+    counts = np.array([w.size for w in want], np.int32)
+    dev = torch.device("cuda", 0)
+    out, so, st = codec.decompress_batch(torch.from_numpy(flat.copy()).to(dev), torch.from_numpy(offs).to(dev),
+                                         torch.from_numpy(sizes).to(dev), torch.from_numpy(counts).to(dev))
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert np.array_equal(out.cpu().numpy()[: counts.sum()], np.concatenate(want))

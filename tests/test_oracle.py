@@ -97,3 +97,12 @@ def test_edge_and_error_behaviour():
     assert O.c5_decompress(blob, 4000)[0] in (O.REMAINING, O.CORRUPT)
     assert O.c5_decompress(blob[:8] + b"\0" + blob[9:], 5000)[0] == O.NOT_ZSTD
     assert O.c5_decompress(blob[:-3], 5000)[0] == O.ZSTD_DECOMPRESS
+
+
+def test_c5_blob_from_other_encoder_settings_round_trips():
+    """The assembled blobs the GPU decoder test uses: the oracle (libzstd reader) inverts them."""
+    for level, wlog in [(3, 0), (19, 0), (1, 10), (19, 11)]:
+        x = O.synth_read(77 + level, 30000)
+        blob = O.c5_assemble([O.zstd_compress_ex(s, level, wlog) for s in O.c5_streams(x)])
+        rc, back = O.c5_decompress(blob, x.size)
+        assert rc == 0 and np.array_equal(back, x), (level, wlog)

@@ -96,3 +96,20 @@ def test_real_c5_streams():
         for arr, sz in zip((keys, S, M, Ll, Lh), sizes):
             s = np.ascontiguousarray(arr[: int(sz)])
             assert model_compress(s) == O.zstd_compress1(s)
+
+
+# frames the reference never writes but any libzstd reader accepts: other levels (compressed FSE
+# sequence tables, 1-stream Huffman literals, long matches) and forced small windows (multi-block
+# frames with repeat-mode tables and offsets into earlier blocks, window-descriptor headers)
+OTHER_SETTINGS = [(3, 0), (9, 0), (19, 0), (-5, 0), (1, 10), (6, 12), (19, 11)]
+
+
+@pytest.mark.parametrize("level,wlog", OTHER_SETTINGS)
+def test_decoder_other_encoder_settings(level, wlog):
+    rng = np.random.default_rng(100 + level * 7 + wlog)
+    for n, kind in [(0, 0), (1, 1), (300, 1), (5000, 2), (40000, 3), (131072, 1), (100000, 2)]:
+        b = gen(rng, n, kind)
+        n = b.size  # generators may return fewer than n bytes
+        fr = O.zstd_compress_ex(b, level, wlog)
+        r, out = model_decompress(fr, n)
+        assert r == n and out == b.tobytes(), (level, wlog, n, kind, r)
