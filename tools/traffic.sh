@@ -1,0 +1,16 @@
+#!/bin/bash
+# HBM traffic of one bench step, per kernel (run on the GPU box).  Two separate --pmc passes
+# (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: MI355X_MICROARCH.md "rocprofv3 PMC
+# slots"), then tools/traffic_summary.py applies the guide's gfx950 FETCH_SIZE correction and
+# writes profiles/traffic_<tag>.json, which bench.py reads into roofline.traffic.
+set -e
+TAG=${1:-latest}
+R=${2:-100000}
+S=${3:-100000}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/traffic
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 400 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/traffic/$C -o run -- \
+      python3 tools/traffic_probe.py $R $S > gpurun_out/traffic/$C.log 2>&1
+done
+python3 tools/traffic_summary.py gpurun_out/traffic $R $S profiles/traffic_$TAG.json

@@ -1,0 +1,36 @@
+"""Per-kernel HBM bytes of one bench step from tools/traffic.sh's two PMC passes.
+
+FETCH_SIZE and WRITE_SIZE are rocprofv3 derived counters in KiB, built from the L2 memory-side
+request counters (TCC_EA0_RDREQ / _WRREQ).  MI355X_MICROARCH.md ("HBM [CDNA4]"): on gfx950
+FETCH_SIZE reports exactly half the bytes of wide coalesced streaming reads, so it is doubled here;
+WRITE_SIZE is taken as is.  Both raw and corrected values are written."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d, R, S, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+val = collections.defaultdict(lambda: collections.defaultdict(float))
+calls = collections.defaultdict(lambda: collections.defaultdict(int))
+for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        k = r["Kernel_Name"].split("(")[0].split()[-1].split("::")[-1]
+        val[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        calls[k][r["Counter_Name"]] += 1
+stages = {"c5_encode": ["enc_split_kernel", "enc_zstd_kernel", "enc_assemble_kernel"],
+          "c5_decode": ["dec_parse_kernel", "dec_zstd_kernel", "dec_merge_kernel"]}
+res = {"reads": R, "samples": S, "unit": "bytes per stage launch (one direction over the whole batch)",
+       "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)", "kernels": {}}
+for k, v in val.items():
+    if not any(k.startswith(p) for p in ("enc_", "dec_")):
+        continue
+    fetch, write = v.get("FETCH_SIZE", 0.0) * 1024, v.get("WRITE_SIZE", 0.0) * 1024
+    res["kernels"][k] = {"fetch_raw": fetch, "write": write, "bytes": 2 * fetch + write,
+                         "dispatches": calls[k].get("FETCH_SIZE", 0)}
+for st, ks in stages.items():
+    if all(k in res["kernels"] for k in ks):
+        res[st] = sum(res["kernels"][k]["bytes"] for k in ks)
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
