@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--cpu-sample-reads", type=int, default=600)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return p.parse_args()
 
 

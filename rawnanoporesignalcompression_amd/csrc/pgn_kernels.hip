@@ -76,7 +76,7 @@ __host__ __device__ inline EncLayout enc_layout()
 }
 
 struct DecLayout {
-    size_t lit, htmp, seqs, tables, bytes;
+    size_t lit, htmp, seqs, tables, htab, xch, bytes;
 };
 __host__ __device__ inline DecLayout dec_layout()
 {
@@ -87,6 +87,8 @@ __host__ __device__ inline DecLayout dec_layout()
     l.htmp = take((size_t)64 * kSliceCap);
     l.seqs = take(12 * (size_t)kMaxDecSeq);
     l.tables = take(4 * ((size_t)kSeqTab + 4));
+    l.htab = take(2u << z1::kHufTableLogMax);
+    l.xch = take(4 * 8 * 64);
     l.bytes = o;
     return l;
 }
@@ -319,6 +321,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.seqs = (uint32_t*)(sbase + lay.seqs);
     S.maxSeq = kMaxDecSeq;
     S.tables = (uint32_t*)(sbase + lay.tables);
+    S.htab = (uint16_t*)(sbase + lay.htab);
+    S.xch = (uint32_t*)(sbase + lay.xch);
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = kStreams * G;
@@ -530,8 +534,8 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&decPerCU, dec_zstd_kernel, 64, 0));
     if (encPerCU < 1) encPerCU = 1;
     if (decPerCU < 1) decPerCU = 1;
-    c->encSlotsMax = (size_t)c->numCUs * (size_t)(encPerCU > 16 ? 16 : encPerCU);
-    c->decSlotsMax = (size_t)c->numCUs * (size_t)(decPerCU > 16 ? 16 : decPerCU);
+    c->encSlotsMax = (size_t)c->numCUs * (size_t)(encPerCU > 32 ? 32 : encPerCU);
+    c->decSlotsMax = (size_t)c->numCUs * (size_t)(decPerCU > 32 ? 32 : decPerCU);
     if (const char* sb = getenv("PGN_SUBBATCH")) {
         long v = atol(sb);
         if (v > 0) c->subBatch = (size_t)v;

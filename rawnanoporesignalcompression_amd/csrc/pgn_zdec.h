@@ -20,15 +20,19 @@ constexpr int kSeqWin = 2048;            // sequences bitstream window staged in
 constexpr int kSeqHdr = 400;             // staged sequences-section header (table descriptions)
 constexpr int kSeqTab = 1280;            // LL [0,512) + OF [512,768) + ML [768,1280) FSE decode entries
 
+constexpr unsigned kHufLdsLog = 11;  // Huffman tables up to this log live in LDS (zstd's encoders
+                                     // never exceed 11); a 12-bit table is built in HBM (slow path)
+
+// Per-workgroup LDS, sized for four decode waves per SIMD: the literal stage (table, boundary
+// bitmap, staging rows) and the sequences stage overlay each other.  A Huffman table that must
+// outlive a sequences stage (treeless literals in a later block) is parked in HBM (DecScratch::htab).
 struct DecLds {
-    uint16_t tab[1 << z1::kHufTableLogMax];  // Huffman decode table: symbol | nbBits << 8
     union {
         struct {  // literals stage
+            uint16_t tab[1u << kHufLdsLog];   // Huffman decode table: symbol | nbBits << 8
             // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
             uint32_t bmp[kBmpBits / 32][64];  // speculative decode: boundary bitmap below each lane start
             uint32_t stg[kStgWords][64];      // staged stream bytes of the current round
-            uint32_t bnd[kBnd / 4][64];       // bytes around each lane's start (phase-2 walk)
-            uint32_t cnt[64], startp[64], endp[64], exitp[64], skip[64], extra[64], obase[64], syncd[64];
             uint8_t wts[256];                 // weights of the current table
             uint8_t order[256];               // symbols sorted by (weight, symbol)
             uint8_t hbuf[272];                // staged Huffman table description (zero padded)
@@ -57,6 +61,8 @@ struct DecScratch {
     uint32_t* seqs;         // decoded sequences: {litLength, matchLength, offset} triples
     uint32_t maxSeq;
     uint32_t* tables;       // the three sequence FSE tables of a multi-block frame (kSeqTab + 4 words)
+    uint16_t* htab;         // 4096 entries: a 12-bit Huffman table, or the parked LDS table
+    uint32_t* xch;          // 8 x 64 words: per-lane values of the serial border walk (rare path)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -88,10 +94,12 @@ __device__ __forceinline__ uint32_t rb_peek(const RevBits& r, int32_t pos, unsig
     if (lo >= r.wlo) return (uint32_t)(r.W >> (lo - r.wlo)) & m;
     return (uint32_t)(r.W << (r.wlo - lo)) & m;  // stream start only (wlo == 0): zero bits below 0
 }
-__device__ __forceinline__ uint32_t rb_huf(RevBits& r, int32_t& pos, unsigned tl)
+// one Huffman symbol; gt = the table in HBM (12-bit tables), null = the LDS table
+__device__ __forceinline__ uint32_t rb_huf(RevBits& r, int32_t& pos, unsigned tl, const uint16_t* gt)
 {
     if (pos - r.wlo < (int32_t)tl && r.wlo > 0) rb_fill(r, pos);
-    const uint32_t e = sDec.tab[rb_peek(r, pos, tl)];
+    const uint32_t ix = rb_peek(r, pos, tl);
+    const uint32_t e = gt ? (uint32_t)gld<uint16_t>(gt + ix) : (uint32_t)sDec.tab[ix];
     pos -= (int32_t)(e >> 8);
     return e & 0xFF;
 }
@@ -285,11 +293,13 @@ __device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxS
     return true;
 }
 
-// Returns header bytes consumed (0 = corrupt); *tlOut = table log.  Fills sDec.tab.
-__device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut)
+// Returns header bytes consumed (0 = corrupt); *tlOut = table log.  Fills sDec.tab, or gt (4096
+// entries in HBM) for a 12-bit table.
+__device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt)
 {
     const int lane = lane_id();
     src = uni(src);
+    gt = uni(gt);
     srcSize = uni((uint64_t)srcSize);
     if (srcSize < 1) return 0;
     // stage the description (at most 129 bytes are part of it)
@@ -450,8 +460,11 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
         if (w > tl || cntW[w] == 0) continue;
         const uint32_t a = rankStart[w], end = a + (cntW[w] << (w - 1));
         const uint16_t nbb = (uint16_t)((tl + 1 - w) << 8);
-        for (uint32_t u = a + (uint32_t)lane; u < end; u += 64)
-            sDec.tab[u] = (uint16_t)(sDec.order[before[w] + ((u - a) >> (w - 1))] | nbb);
+        for (uint32_t u = a + (uint32_t)lane; u < end; u += 64) {
+            const uint16_t e = (uint16_t)(sDec.order[before[w] + ((u - a) >> (w - 1))] | nbb);
+            if (tl <= kHufLdsLog) sDec.tab[u] = e;
+            else gst<uint16_t>(gt + u, e);
+        }
     }
     lds_sync();
     *tlOut = tl;
@@ -467,36 +480,47 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
 // point are written by the walker.  Finally every lane copies its synchronised symbols into place
 // (phase 3).  Returns false on a malformed stream.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint8_t bnd_byte(int l, int32_t b) { return ((const uint8_t*)&sDec.bnd[b >> 2][l])[b & 3]; }
-
-// the walker's bit peek: from the lane's cached border bytes when they cover [q - tl, q)
-__device__ __forceinline__ uint32_t walk_peek(int l, int32_t Sl, const uint8_t* s, int32_t sl, int32_t q, unsigned tl)
+// the walker's bit peek over HBM: the tl bits below q (bits below the stream start read as zero)
+__device__ __forceinline__ uint32_t walk_peek_g(const uint8_t* s, int32_t sl, int32_t q, unsigned tl)
 {
     const int32_t lo = q - (int32_t)tl;
     const uint32_t mask = (1u << tl) - 1u;
-    if (lo < 0) {  // bits below the stream start read as zero
+    if (lo < 0) {
         uint32_t v = 0;
         for (int k = 0; k < 2; k++)
             if (k < sl) v |= (uint32_t)gb(s + k) << (8 * k);
         v &= (1u << q) - 1u;
         return (v << (-lo)) & mask;
     }
-    const int32_t b0 = (Sl >> 3) - kBndBelow;
-    const int32_t i0 = (lo >> 3) - b0;
-    uint32_t v;
-    if (i0 >= 0 && i0 + 2 < kBnd) {
-        v = (uint32_t)bnd_byte(l, i0) | ((uint32_t)bnd_byte(l, i0 + 1) << 8) | ((uint32_t)bnd_byte(l, i0 + 2) << 16);
-    } else {
-        const int32_t b = lo >> 3;
-        v = 0;
-        for (int k = 0; k < 3; k++)
-            if (b + k < sl) v |= (uint32_t)gb(s + b + k) << (8 * k);
-    }
+    const int32_t b = lo >> 3;
+    uint32_t v = 0;
+    for (int k = 0; k < 3; k++)
+        if (b + k < sl) v |= (uint32_t)gb(s + b + k) << (8 * k);
     return (v >> (lo & 7)) & mask;
 }
 
+// the same from the lane's own border bytes [Sl/8 - kBndBelow, Sl/8 - kBndBelow + kBnd), kept in
+// registers, when they cover [q - tl, q)
+__device__ __forceinline__ uint32_t bw_word(const uint32_t (&bw)[kBnd / 4], int32_t w)
+{
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < kBnd / 4; i++) v = (w == i) ? bw[i] : v;
+    return v;
+}
+__device__ __forceinline__ uint32_t walk_peek_own(const uint32_t (&bw)[kBnd / 4], int32_t Sl, const uint8_t* s, int32_t sl,
+                                                  int32_t q, unsigned tl)
+{
+    const int32_t lo = q - (int32_t)tl;
+    const int32_t i0 = (lo >> 3) - ((Sl >> 3) - kBndBelow);
+    if (lo < 0 || i0 < 0 || i0 + 2 >= kBnd) return walk_peek_g(s, sl, q, tl);
+    const int32_t w = i0 >> 2;
+    const uint64_t v = (uint64_t)bw_word(bw, w) | ((uint64_t)bw_word(bw, w + 1) << 32);
+    return (uint32_t)(v >> (8 * (i0 & 3) + (lo & 7))) & ((1u << tl) - 1u);
+}
+
 __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                              uint8_t* htmp, PhaseProf& P)
+                                              uint8_t* htmp, uint32_t* xch, PhaseProf& P)
 {
     const int lane = lane_id();
     tl = uni(tl);
@@ -505,6 +529,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     dst = uni(dst);
     rs = uni(rs);
     htmp = uni(htmp);
+    xch = uni(xch);
     const int k = lane >> 4, j = lane & 15;
     if (remain < 6) return false;
     const size_t l1 = gld<uint16_t>(hp), l2 = gld<uint16_t>(hp + 2), l3 = gld<uint16_t>(hp + 4);
@@ -523,13 +548,11 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     const int32_t S = (B > j * Lr) ? B - j * Lr : 0;
     const int32_t E = (B > (j + 1) * Lr) ? B - (j + 1) * Lr : 0;
     // border bytes for the walk
+    uint32_t bw[kBnd / 4];
     {
         const int32_t b0 = (S >> 3) - kBndBelow;
 #pragma unroll
-        for (int w = 0; w < kBnd / 4; w++) {
-            const uint32_t v = ld_word(src, sl, b0 + 4 * w);
-            sDec.bnd[w][lane] = v;
-        }
+        for (int w = 0; w < kBnd / 4; w++) bw[w] = ld_word(src, sl, b0 + 4 * w);
     }
     // ---- phase 1: speculative decode of (E, S] into the lane's slice
 #pragma unroll
@@ -624,11 +647,6 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     }
     const uint32_t c = stored + npend;
     P.mark(11);
-    sDec.cnt[lane] = c;
-    sDec.startp[lane] = (uint32_t)S;
-    sDec.endp[lane] = (uint32_t)E;
-    sDec.exitp[lane] = (uint32_t)q;
-    lds_sync();
     // ---- phase 2: the border walks.  If lane l-1 synchronised, the true path enters lane l's range
     // at l-1's speculative exit, so all 15 walks of a stream run at once; the walk symbols wait in
     // the (now free) staging row.  A stream with a lane that does not meet its boundaries within
@@ -637,14 +655,15 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     auto wsym_at = [&](uint32_t t) -> uint8_t& { return ((uint8_t*)&sDec.stg[t >> 2][lane])[t & 3]; };
     constexpr uint32_t kWalkMax = 4 * kStgWords;
     uint32_t ex = 0;
-    int32_t p = (j == 0) ? S : (int32_t)sDec.exitp[lane - 1];
+    const int32_t prevExit = (int32_t)dpp<kDppRowShr1>((uint32_t)q);  // lane l-1's exit (rows = streams)
+    int32_t p = (j == 0) ? S : prevExit;
     bool synced = (j == 0);
     if (j > 0) {
         while (p > E && ex < kWalkMax) {
             const int32_t d = S - p;
             if (d >= kBmpBits) break;
             if ((sDec.bmp[d >> 5][lane] >> (d & 31)) & 1u) { synced = true; break; }
-            const uint32_t e = sDec.tab[walk_peek(lane, S, src, sl, p, tl)];
+            const uint32_t e = sDec.tab[walk_peek_own(bw, S, src, sl, p, tl)];
             p -= (int32_t)(e >> 8);
             wsym_at(ex++) = (uint8_t)e;
         }
@@ -658,80 +677,93 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     const uint64_t unsynced = ballot(!synced);
     const bool fast = ((unsynced >> (16 * k)) & 0xFFFFull) == 0;
     uint8_t* sdst = dst + (size_t)seg * (size_t)k;
-    if (fast) {
+    // this lane's placement: skip its first sk speculative symbols, write exl walk symbols at ob
+    uint32_t sk = idx, syncd = (uint32_t)dsync, exl = ex, ob = 0;
+    {
         const uint32_t tc = ex + (c - idx);
         uint32_t incl = tc;  // inclusive sum over the stream's 16 lanes (one DPP row)
         incl += dpp<kDppRowShr1>(incl);
         incl += dpp<kDppRowShr2>(incl);
         incl += dpp<kDppRowShr4>(incl);
         incl += dpp<kDppRowShr8>(incl);
-        sDec.skip[lane] = idx;
-        sDec.syncd[lane] = (uint32_t)dsync;
-        sDec.extra[lane] = ex;
-        sDec.obase[lane] = incl - tc;
-        if (j == 15) {
+        ob = incl - tc;
+        if (fast && j == 15) {
             sDec.u[8 + k] = incl;
             sDec.u[12 + k] = (uint32_t)q;  // true end of the stream (must be 0)
         }
     }
-    lds_sync();
-    // serial fallback: one lane per stream walks the 15 borders in order
-    if (!fast && j == 0) {
-        sDec.skip[lane] = 0;
-        sDec.syncd[lane] = 0;
-        sDec.extra[lane] = 0;
-        sDec.obase[lane] = 0;
-        uint32_t out = c;  // symbols placed so far in this stream
-        int32_t T = q;
-        for (int jj = 1; jj < 16; jj++) {
-            const int l = lane + jj;
-            const uint32_t cl = sDec.cnt[l];
-            const int32_t Sl = (int32_t)sDec.startp[l], El = (int32_t)sDec.endp[l];
-            sDec.obase[l] = out;
-            int32_t pp = T;
-            uint32_t exx = 0;
-            bool sy = false;
-            while (pp > El) {
-                const int32_t d = Sl - pp;
-                if (d >= kBmpBits) break;  // past the recorded boundaries: finish serially below
-                if ((sDec.bmp[d >> 5][l] >> (d & 31)) & 1u) { sy = true; break; }
-                const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, pp, tl)];
-                pp -= (int32_t)(e >> 8);
-                if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
-                exx++;
-            }
-            if (sy) {
-                const int32_t d = Sl - pp;
-                uint32_t ix = 0;
-                for (int w = 0; w < (d >> 5); w++) ix += (uint32_t)__builtin_popcount(sDec.bmp[w][l]);
-                if (d & 31) ix += (uint32_t)__builtin_popcount(sDec.bmp[d >> 5][l] & ((1u << (d & 31)) - 1u));
-                sDec.skip[l] = ix;
-                sDec.syncd[l] = (uint32_t)d;
-                T = (int32_t)sDec.exitp[l];
-                out += exx + (cl - ix);
-            } else {  // no common boundary: the walker decodes the rest of the range itself
+    if (unsynced) {
+        // serial fallback: one lane per such stream walks the 15 borders in order, over the lanes'
+        // values exchanged through HBM (a wave's vector-memory accesses are performed in order)
+        uint32_t* X = xch;
+        X[lane] = c;
+        X[64 + lane] = (uint32_t)S;
+        X[128 + lane] = (uint32_t)E;
+        X[192 + lane] = (uint32_t)q;
+        wave_sync();
+        if (!fast && j == 0) {
+            X[256 + lane] = 0;  // obase, skip, syncd, extra of the stream's first lane
+            X[320 + lane] = 0;
+            X[384 + lane] = 0;
+            X[448 + lane] = 0;
+            uint32_t out = c;  // symbols placed so far in this stream
+            int32_t T = q;
+            for (int jj = 1; jj < 16; jj++) {
+                const int l = lane + jj;
+                const uint32_t cl = X[l];
+                const int32_t Sl = (int32_t)X[64 + l], El = (int32_t)X[128 + l];
+                X[256 + l] = out;
+                int32_t pp = T;
+                uint32_t exx = 0;
+                bool sy = false;
                 while (pp > El) {
-                    const uint32_t e = sDec.tab[walk_peek(l, Sl, src, sl, pp, tl)];
+                    const int32_t d = Sl - pp;
+                    if (d >= kBmpBits) break;  // past the recorded boundaries: finish serially below
+                    if ((sDec.bmp[d >> 5][l] >> (d & 31)) & 1u) { sy = true; break; }
+                    const uint32_t e = sDec.tab[walk_peek_g(src, sl, pp, tl)];
                     pp -= (int32_t)(e >> 8);
                     if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
                     exx++;
                 }
-                sDec.skip[l] = cl;
-                T = pp;
-                out += exx;
+                if (sy) {
+                    const int32_t d = Sl - pp;
+                    uint32_t ix = 0;
+                    for (int w = 0; w < (d >> 5); w++) ix += (uint32_t)__builtin_popcount(sDec.bmp[w][l]);
+                    if (d & 31) ix += (uint32_t)__builtin_popcount(sDec.bmp[d >> 5][l] & ((1u << (d & 31)) - 1u));
+                    X[320 + l] = ix;
+                    X[384 + l] = (uint32_t)d;
+                    T = (int32_t)X[192 + l];
+                    out += exx + (cl - ix);
+                } else {  // no common boundary: the walker decodes the rest of the range itself
+                    while (pp > El) {
+                        const uint32_t e = sDec.tab[walk_peek_g(src, sl, pp, tl)];
+                        pp -= (int32_t)(e >> 8);
+                        if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
+                        exx++;
+                    }
+                    X[320 + l] = cl;
+                    X[384 + l] = 0;
+                    T = pp;
+                    out += exx;
+                }
+                X[448 + l] = exx;
             }
-            sDec.extra[l] = exx;
+            sDec.u[12 + k] = (uint32_t)T;
+            sDec.u[8 + k] = out;
         }
-        sDec.u[12 + k] = (uint32_t)T;
-        sDec.u[8 + k] = out;
+        wave_sync();
+        if (!fast) {
+            ob = X[256 + lane];
+            sk = X[320 + lane];
+            syncd = X[384 + lane];
+            exl = X[448 + lane];
+        }
     }
     lds_sync();
     P.mark(12);
     const bool good = (sDec.u[8 + k] == nsym) && ((int32_t)sDec.u[12 + k] == 0);
     if (ballot(!good)) return false;
     // ---- phase 3: walk symbols and the synchronised speculative symbols into place
-    const uint32_t sk = sDec.skip[lane];
-    const uint32_t ob = sDec.obase[lane], exl = sDec.extra[lane];
     if (fast)
         for (uint32_t t = 0; t < exl; t++) gst<uint8_t>(sdst + ob + t, wsym_at(t));
     const uint32_t o = ob + exl;
@@ -751,7 +783,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             for (; t + 4 <= len; t += 4) gst<uint32_t>(to + t, gld<uint32_t>(from + t));
             for (; t < len; t++) gst<uint8_t>(to + t, gb(from + t));
         } else {  // slice overflow: decode again from the synchronisation point
-            int32_t pp = S - (int32_t)sDec.syncd[lane];
+            int32_t pp = S - (int32_t)syncd;
             GBits g;
             gbits_init(g, src, sl, pp);
             for (uint32_t t = 0; t < len; t++) {
@@ -764,15 +796,43 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     return true;
 }
 
+// Four streams with a 12-bit table (HBM): one lane per stream decodes serially.  zstd's own
+// encoders never write such tables; this path exists for completeness of the format.
+__device__ __noinline__ bool huf_decode1_lane(unsigned tl, const uint8_t* src, size_t sl, uint8_t* dst, uint32_t n,
+                                              const uint16_t* gt);
+__device__ __noinline__ bool huf_decode4_serial(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
+                                                const uint16_t* gt)
+{
+    const int lane = lane_id();
+    hp = uni(hp);
+    remain = uni((uint64_t)remain);
+    if (remain < 6) return false;
+    const size_t l1 = gld<uint16_t>(hp), l2 = gld<uint16_t>(hp + 2), l3 = gld<uint16_t>(hp + 4);
+    if (l1 + l2 + l3 + 6 > remain) return false;
+    const size_t l4 = remain - 6 - l1 - l2 - l3;
+    const uint32_t seg = (rs + 3) / 4;
+    if (seg * 3 > rs) return false;
+    bool ok = true;
+    if ((lane & 15) == 0) {
+        const int k = lane >> 4;
+        const size_t so = (k == 0) ? 0 : (k == 1 ? l1 : (k == 2 ? l1 + l2 : l1 + l2 + l3));
+        const size_t sl = (k == 0) ? l1 : (k == 1 ? l2 : (k == 2 ? l3 : l4));
+        const uint32_t nsym = (k == 3) ? rs - 3 * seg : seg;
+        ok = huf_decode1_lane(tl, hp + 6 + so, sl, dst + (size_t)seg * k, nsym, gt);
+    }
+    return ballot(!ok) == 0;
+}
+
 // single-stream literals (< 256 symbols in zstd's encoder): lane 0
-__device__ __noinline__ bool huf_decode1_lane(unsigned tl, const uint8_t* src, size_t sl, uint8_t* dst, uint32_t n)
+__device__ __noinline__ bool huf_decode1_lane(unsigned tl, const uint8_t* src, size_t sl, uint8_t* dst, uint32_t n,
+                                              const uint16_t* gt)
 {
     if (sl == 0 || gb(src + sl - 1) == 0) return false;
     int32_t pos = (int32_t)(sl - 1) * 8 + (int32_t)z1::highbit32(gb(src + sl - 1));
     RevBits rb;
     rb.s = src;
     rb_fill(rb, pos);
-    for (uint32_t i = 0; i < n; i++) gst<uint8_t>(dst + i, (uint8_t)rb_huf(rb, pos, tl));
+    for (uint32_t i = 0; i < n; i++) gst<uint8_t>(dst + i, (uint8_t)rb_huf(rb, pos, tl, gt));
     return pos == 0;
 }
 
@@ -1097,6 +1157,8 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     S.seqs = uni(S.seqs);
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
+    S.htab = uni(S.htab);
+    S.xch = uni(S.xch);
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
     while (ip < srcSize) {
@@ -1131,7 +1193,9 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
         hpos += fcsSize;
         ip = hpos;
         const size_t frameStart = op;
-        bool hufValid = false;
+        bool hufValid = false;  // a Huffman table exists for treeless literals
+        bool hufInLds = false;  // ... and is in sDec.tab (tables up to kHufLdsLog)
+        bool hufParked = false; // ... and a copy is parked in S.htab
         unsigned hufTl = 0;
         if (lane == 0) {  // frame state of the sequences stage: repeat offsets, table validity
             sDec.u[2] = 1;
@@ -1204,21 +1268,30 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     size_t remain = cs;
                     if (ltype == z1::kSetCompressed) {
                         unsigned tlNew = 0;
-                        const size_t hsz = huf_build_dtable_wave(hp, remain, &tlNew);
+                        const size_t hsz = huf_build_dtable_wave(hp, remain, &tlNew, S.htab);
                         P.mark(1);
                         if (hsz == 0) return z1::kDecErrHufTable;
                         hufValid = true;
                         hufTl = tlNew;
+                        hufInLds = tlNew <= kHufLdsLog;
+                        hufParked = !hufInLds;
                         hp += hsz;
                         remain -= hsz;
                     } else if (!hufValid) {
                         return z1::kDecErrCorrupt;
+                    } else if (!hufInLds && hufTl <= kHufLdsLog) {  // bring the parked table back
+                        for (uint32_t i = (uint32_t)lane; i < (1u << hufTl); i += 64) sDec.tab[i] = gld<uint16_t>(S.htab + i);
+                        hufInLds = true;
+                        lds_sync();
                     }
+                    const uint16_t* gt = (hufTl <= kHufLdsLog) ? nullptr : S.htab;
                     bool ok = true;
                     if (single) {
-                        if (lane == 0) ok = huf_decode1_lane(hufTl, hp, remain, litOut, (uint32_t)rs);
+                        if (lane == 0) ok = huf_decode1_lane(hufTl, hp, remain, litOut, (uint32_t)rs, gt);
+                    } else if (gt) {
+                        ok = huf_decode4_serial(hufTl, hp, remain, litOut, (uint32_t)rs, gt);
                     } else {
-                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, S.htmp, P);
+                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, S.htmp, S.xch, P);
                     }
                     if (ballot(!ok)) return z1::kDecErrHufStream;
                     P.mark(2);
@@ -1227,6 +1300,13 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                 if (noSeq) {
                     op += rs;
                 } else {
+                    // the sequences stage overlays sDec.tab: park the table if a later block may reuse it
+                    if (!last && hufInLds && !hufParked) {
+                        for (uint32_t i = (uint32_t)lane; i < (1u << hufTl); i += 64) gst<uint16_t>(S.htab + i, sDec.tab[i]);
+                        hufParked = true;
+                    }
+                    hufInLds = false;
+                    wave_sync();
                     const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, last != 0);
                     if (r < 0) return r;
                     op = (size_t)r;

@@ -33,25 +33,33 @@ struct EncLds {
             uint64_t filt[kFiltSlots];
             uint32_t vh0[64], vh1[64], vpk[64];
         };
-        struct {  // literals
-            uint32_t hist2[2][256];  // per-segment histograms, two 16-bit counts per word
-            uint32_t count[256];
-            uint32_t cw[256];  // Huffman code | nbBits << 16
-            z1::HufNode nodes[2 * 256 + 4];
-            uint8_t nbBits[256];
+        struct {  // literals; members grouped by lifetime so that each phase's scratch overlays the last
+            uint32_t hist2[2][256];  // per-segment histograms, two 16-bit counts per word (histogram -> stream sizes)
+            union {
+                uint32_t count[256];  // histogram -> sort
+                uint32_t cw[256];     // Huffman code | nbBits << 16 (stream sizes -> encode)
+            };
+            uint8_t nbBits[256];  // tree -> stream sizes
             uint16_t val[256];
-            uint8_t weights[256];
-            uint8_t hdr[256];  // Huffman table description (the FSE form may run to ~210 bytes before it is rejected)
-            WCTable fct;
-            uint8_t fscratch[64];
-            uint32_t win[kWinWords];
-            uint16_t tanc[256];  // tree depths by pointer jumping: ancestor of internal node 256 + i
-            uint16_t tdep[256];  //                                 distance to it
-            uint32_t rankLast[16];
-            uint32_t vpr[16];     // valPerRank
-            uint32_t wcount[16];  // weight histogram
-            int16_t wnorm[16];
-            uint32_t wcumul[16];
+            union {
+                struct {  // tree build
+                    z1::HufNode nodes[2 * 256 + 4];
+                    uint16_t tanc[256];  // tree depths by pointer jumping: ancestor of internal node 256 + i
+                    uint16_t tdep[256];  //                                 distance to it
+                    uint32_t rankLast[16];
+                    uint32_t vpr[16];  // valPerRank
+                };
+                struct {  // table description
+                    uint8_t weights[256];
+                    uint8_t hdr[256];  // Huffman table description (the FSE form may run to ~210 bytes before it is rejected)
+                    WCTable fct;
+                    uint8_t fscratch[64];
+                    uint32_t wcount[16];  // weight histogram
+                    int16_t wnorm[16];
+                    uint32_t wcumul[16];
+                };
+                uint32_t win[kWinWords];  // encode: output bit window
+            };
         };
         struct {  // sequences section (after the literals section is written)
             z1::FseCTable sct[3];  // ll, of, ml
