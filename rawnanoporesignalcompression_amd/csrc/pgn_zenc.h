@@ -173,21 +173,44 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
     lds_sync();
-    while (ip0 + 1 < ilimit) {
-        // positions of the next 64 visits (the no-match recurrence), scalar
-        int32_t q = ip0;
-        int32_t pk = 0;
+    // positions of the 64 visits starting at p (the no-match recurrence; scalar, with v_writelane)
+    auto positions = [&](int32_t p, int32_t& pkOut, int32_t& pNextOut) {
+        int32_t q = p, pk = 0;
+#pragma unroll
         for (int k = 0; k < 64; k++) {
-            pk = ((int)lane == k) ? q : pk;
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(pk) : "s"(q), "i"(k));
             q += ((q - anchor) >> 7) + 2;
         }
-        const int32_t pNext = q;
+        pkOut = pk;
+        pNextOut = q;
+    };
+    int32_t pk = 0, pNext = 0;
+    uint64_t v8 = 0;    // bytes pk .. pk+7: both hashes and the current-position words
+    uint32_t repw = 0;  // bytes at pk + 2 - off1 (repcode candidate)
+    auto loads = [&](int32_t p, uint64_t& v, uint32_t& r) {
+        if (p + 1 < ilimit) {
+            v = ld64u(src + p);
+            r = (off1 > 0) ? ld32u(src + p + 2 - (int32_t)off1) : 0u;
+        }
+    };
+    bool havePk = false;  // pk / pNext / v8 / repw already hold this round's visits (from the last round)
+    while (ip0 + 1 < ilimit) {
+        if (!havePk) {
+            positions(ip0, pk, pNext);
+            loads(pk, v8, repw);
+        }
+        havePk = false;
         const bool valid = (pk + 1 < ilimit);
         uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu, t0 = 0, t1 = 0;
         uint64_t M0 = 0, M1 = 0;
         if (valid) {
-            h0 = hash_g(src + pk, hlog, mls);
-            h1 = hash_g(src + pk + 1, hlog, mls);
+            if (mls == 5) {
+                h0 = (uint32_t)(((v8 << 24) * 889523592379ull) >> (64 - hlog));
+                h1 = (uint32_t)((((v8 >> 8) << 24) * 889523592379ull) >> (64 - hlog));
+            } else {
+                h0 = (uint32_t)(((v8 << 16) * 227718039650203ull) >> (64 - hlog));
+                h1 = (uint32_t)((((v8 >> 8) << 16) * 227718039650203ull) >> (64 - hlog));
+            }
             t0 = gld<uint32_t>(ht + h0);
             t1 = gld<uint32_t>(ht + h1);
             atomicOr((unsigned long long*)&L.filt[h0 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
@@ -196,6 +219,13 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
         L.vh0[lane] = h0;
         L.vh1[lane] = h1;
         L.vpk[lane] = (uint32_t)pk;
+        // the next round's visits and their bytes, assuming this one finds no match (overlaps the
+        // table reads)
+        int32_t pkN, pNextN;
+        positions(pNext, pkN, pNextN);
+        uint64_t v8N = 0;
+        uint32_t repwN = 0;
+        loads(pkN, v8N, repwN);
         lds_sync();
         if (valid) {
             M0 = L.filt[h0 & (kFiltSlots - 1)];
@@ -225,11 +255,9 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
         }
         bool rep = false, c0 = false, c1 = false;
         if (valid) {
-            const int32_t ip2 = pk + 2;
-            const uint32_t here = ld32u(src + pk + 1);  // bytes pk+1 .. pk+4
-            rep = (off1 > 0) && (ld32u(src + ip2 - (int32_t)off1) == ld32u(src + ip2));
-            c0 = (m0 > 1) && (ld32u(src + m0 - 1) == ld32u(src + pk));
-            c1 = (m1 > 1) && (ld32u(src + m1 - 1) == here);
+            rep = (off1 > 0) && (repw == (uint32_t)(v8 >> 16));
+            c0 = (m0 > 1) && (ld32u(src + m0 - 1) == (uint32_t)v8);
+            c1 = (m1 > 1) && (ld32u(src + m1 - 1) == (uint32_t)(v8 >> 8));
         }
         const uint64_t hits = ballot(rep || c0 || c1);
         const uint64_t vmask = ballot(valid);
@@ -255,7 +283,15 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
         lds_sync();
         if (!hits) {
             wave_sync();
-            if (vmask == ~0ull) { ip0 = pNext; continue; }
+            if (vmask == ~0ull) {
+                ip0 = pNext;
+                pk = pkN;
+                pNext = pNextN;
+                v8 = v8N;
+                repw = repwN;
+                havePk = true;
+                continue;
+            }
             break;
         }
         // the match found at visit f, processed exactly as the serial loop does
@@ -769,34 +805,77 @@ __device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t
                 const size_t nh = z1::fse_write_ncount(L.hdr + 1, L.wnorm, maxW, tableLog);
                 if (nh && wtSize > 2) {
                     fse_build_ctable_small(L.fct, L.wnorm, maxW, tableLog, L.fscratch, L.wcumul);
-                    uint8_t* op = L.hdr + 1 + nh;
-                    z1::BitW bw;
-                    z1::bw_init(bw, op);
-                    const uint8_t* ip = L.weights + wtSize;
+                    // FSE_compress_usingCTable (two interleaved states), wave-uniform over registers:
+                    // table entry u / symbol s in lane u / s (read with v_readlane), weight of symbol
+                    // i in lane i & 63 of w[i >> 6]; the bitstream collects as 32-bit words in lane
+                    // order (<= 255 * 6 bits).
+                    const uint32_t vST = ((uint32_t)lane < (1u << tableLog)) ? (uint32_t)L.fct.stateTable[lane] : 0u;
+                    const uint32_t vDN = ((uint32_t)lane <= maxW) ? L.fct.deltaNbBits[lane] : 0u;
+                    const uint32_t vDF = ((uint32_t)lane <= maxW) ? (uint32_t)L.fct.deltaFindState[lane] : 0u;
+                    auto wsym = [&](uint32_t i) -> uint32_t {
+                        const uint32_t r = i >> 6;
+                        const uint32_t v = r == 0 ? w[0] : (r == 1 ? w[1] : (r == 2 ? w[2] : w[3]));
+                        return readlane_u32(v, (int)(i & 63u));
+                    };
+                    uint32_t wv = 0, nw = 0, nacc = 0;
+                    uint64_t acc = 0;
+                    auto put = [&](uint32_t v, uint32_t nb) {  // nb <= 7
+                        acc |= (uint64_t)(v & ((1u << nb) - 1u)) << nacc;
+                        nacc += nb;
+                        if (nacc >= 32) {
+                            wv = ((uint32_t)lane == nw) ? (uint32_t)acc : wv;
+                            nw++;
+                            acc >>= 32;
+                            nacc -= 32;
+                        }
+                    };
+                    auto init = [&](uint32_t sym) -> uint32_t {
+                        const uint32_t dn = readlane_u32(vDN, (int)sym), df = readlane_u32(vDF, (int)sym);
+                        const uint32_t nbo = (dn + (1u << 15)) >> 16;
+                        const uint32_t v = (nbo << 16) - dn;
+                        return readlane_u32(vST, (int)((v >> nbo) + df));
+                    };
+                    auto enc = [&](uint32_t& st, uint32_t sym) {
+                        const uint32_t dn = readlane_u32(vDN, (int)sym), df = readlane_u32(vDF, (int)sym);
+                        const uint32_t nbo = (st + dn) >> 16;
+                        put(st, nbo);
+                        st = readlane_u32(vST, (int)((st >> nbo) + df));
+                    };
+                    uint32_t ip = wtSize;
                     uint32_t s1, s2;
-                    size_t left = wtSize;
-                    if (left & 1) {
-                        wfse_init(s1, L.fct, *--ip);
-                        wfse_init(s2, L.fct, *--ip);
-                        wfse_encode(bw, s1, L.fct, *--ip);
+                    if (wtSize & 1) {
+                        s1 = init(wsym(ip - 1));
+                        s2 = init(wsym(ip - 2));
+                        enc(s1, wsym(ip - 3));
+                        ip -= 3;
                     } else {
-                        wfse_init(s2, L.fct, *--ip);
-                        wfse_init(s1, L.fct, *--ip);
+                        s2 = init(wsym(ip - 1));
+                        s1 = init(wsym(ip - 2));
+                        ip -= 2;
                     }
-                    left -= 2;
-                    if (left & 2) {
-                        wfse_encode(bw, s2, L.fct, *--ip);
-                        wfse_encode(bw, s1, L.fct, *--ip);
+                    if ((wtSize - 2) & 2) {
+                        enc(s2, wsym(ip - 1));
+                        enc(s1, wsym(ip - 2));
+                        ip -= 2;
                     }
-                    while (ip > L.weights) {
-                        wfse_encode(bw, s2, L.fct, *--ip);
-                        wfse_encode(bw, s1, L.fct, *--ip);
-                        wfse_encode(bw, s2, L.fct, *--ip);
-                        wfse_encode(bw, s1, L.fct, *--ip);
+                    while (ip > 0) {
+                        enc(s2, wsym(ip - 1));
+                        enc(s1, wsym(ip - 2));
+                        enc(s2, wsym(ip - 3));
+                        enc(s1, wsym(ip - 4));
+                        ip -= 4;
                     }
-                    z1::bw_add(bw, s2, L.fct.tableLog);
-                    z1::bw_add(bw, s1, L.fct.tableLog);
-                    hSize = (uint32_t)(nh + z1::bw_close(bw, op));
+                    put(s2, tableLog);
+                    put(s1, tableLog);
+                    put(1, 1);  // end mark
+                    const uint32_t tailBytes = (nacc + 7) >> 3;
+                    uint8_t* op = L.hdr + 1 + nh;
+                    if ((uint32_t)lane < nw) {
+#pragma unroll
+                        for (int b = 0; b < 4; b++) op[4 * lane + b] = (uint8_t)(wv >> (8 * b));
+                    }
+                    if ((uint32_t)lane < tailBytes) op[4 * nw + lane] = (uint8_t)(acc >> (8 * lane));
+                    hSize = (uint32_t)(nh + 4 * nw + tailBytes);
                 }
             }
         }
@@ -1208,7 +1287,6 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
 __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
                                              EncScratch S, uint32_t tag, PhaseProf& P)
 {
-    EncLds& L = sEnc;
     dst = uni(dst);
     src = uni(src);
     n = uni(n);

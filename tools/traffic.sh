@@ -2,7 +2,7 @@
 # HBM traffic of one bench step, per kernel (run on the GPU box).  Two separate --pmc passes
 # (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: MI355X_MICROARCH.md "rocprofv3 PMC
 # slots"), then tools/traffic_summary.py applies the guide's gfx950 FETCH_SIZE correction and
-# writes profiles/traffic_<tag>.json, which bench.py reads into roofline.traffic.
+# writes gpurun_out/traffic_<tag>.json; copied to profiles/, bench.py reads it into roofline.traffic.
 set -e
 TAG=${1:-latest}
 R=${2:-100000}
@@ -13,4 +13,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/traffic/$C -o run -- \
       python3 tools/traffic_probe.py $R $S > gpurun_out/traffic/$C.log 2>&1
 done
-python3 tools/traffic_summary.py gpurun_out/traffic $R $S profiles/traffic_$TAG.json
+python3 tools/traffic_summary.py gpurun_out/traffic $R $S gpurun_out/traffic_$TAG.json  # copied into profiles/ to commit
