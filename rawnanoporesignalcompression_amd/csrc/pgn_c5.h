@@ -20,21 +20,22 @@ struct C5Streams {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Split.  A step is 1024 samples; sub-step k gives lane l sample t + 64k + l.  The class of every
-// sample becomes three wave ballots; a value's place in its stream is the stream's fill plus the
-// number of same-class lanes below it (mbcnt), so each lane writes its byte straight into an LDS
-// window.  Keys are OR-ed across lane quads with DPP.  After a step, complete 16-byte blocks of
+// Split.  A step is 1024 samples; lane l takes the 16 consecutive samples t + 16l .. t + 16l + 15,
+// so its 16 keys are one key word.  A value's place in its stream is the stream's fill plus the
+// class counts of the lanes below (one packed DPP scan) plus its rank among the lane's own
+// samples, so each lane writes its bytes straight into LDS windows (bytes of other classes go to
+// a per-lane dummy slot instead of being predicated).  After a step, complete 16-byte blocks of
 // each window go to HBM as aligned 16-byte stores and the tail moves to the window front.
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kSplitStep = 1024;
 constexpr uint32_t kWinBytes = 1088;  // 31 carried nibbles + 1024 new, rounded up to 16
+constexpr uint32_t kDummy = kWinBytes;  // + 4 * lane: per-lane discard slots (distinct banks)
 
 struct SplitLds {
-    alignas(16) uint8_t S[kWinBytes];  // one byte per nibble
-    alignas(16) uint8_t M[kWinBytes];
+    alignas(16) uint8_t S[kWinBytes + 256];  // one byte per nibble
+    alignas(16) uint8_t M[kWinBytes + 256];
     alignas(16) uint8_t L[kWinBytes];
     alignas(16) uint8_t H[kWinBytes];
-    alignas(16) uint8_t K[kSplitStep / 4];
 };
 
 // 4 nibble-bytes (each < 16) -> their 16-bit little-endian nibble packing
@@ -80,51 +81,74 @@ __device__ __forceinline__ void nwin_flush(uint8_t* W, uint32_t& fill, uint8_t* 
     fill = tail;
 }
 
-// One 1024-sample step (Full: every sample of the step exists).  Per sub-step: three compares give
-// the class ballots (classes combined in scalar registers), each class's bytes go to its window
-// at fill + mbcnt rank under that class's exec mask (class 3 is rare and usually skipped whole),
-// and the quad-OR-ed key byte is written by all four lanes of a quad (same byte, no masking).
+// One 1024-sample step (Full: every sample of the step exists).  Returns the lane's key word.
 template <bool Full>
-__device__ __forceinline__ void split_step(const int16_t* __restrict__ x, uint32_t n, uint32_t t, SplitLds& W,
-                                           uint32_t& fS, uint32_t& fM, uint32_t& fL, uint32_t& prevX)
+__device__ __forceinline__ uint32_t split_step(const int16_t* __restrict__ x, uint32_t n, uint32_t t, SplitLds& W,
+                                               uint32_t& fS, uint32_t& fM, uint32_t& fL, uint32_t& prevX)
 {
     const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t i0 = t + 16u * lane;
     uint32_t xv[16];
+    if (Full) {
+        const uint4 a = gld<uint4>(x + i0), b = gld<uint4>(x + i0 + 8);
+        const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int k = 0; k < 16; k++) {  // a partial step re-reads the last sample (masked below)
-        const uint32_t i = t + 64u * (uint32_t)k + lane;
-        xv[k] = (uint32_t)gld<uint16_t>(x + (Full ? i : (i < n ? i : n - 1)));
+        for (int k = 0; k < 8; k++) {
+            xv[2 * k] = wd[k] & 0xFFFFu;
+            xv[2 * k + 1] = wd[k] >> 16;
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < 16; m++) xv[m] = (i0 + (uint32_t)m < n) ? (uint32_t)gld<uint16_t>(x + i0 + m) : 0u;
     }
-    const uint32_t ksh = 2u * (lane & 3u);
+    // the sample before mine: lane l-1's last one (lane 0: the previous step's)
+    uint32_t prv = dpp<kDppWaveShr1>(xv[15]);
+    prv = (lane == 0) ? prevX : prv;
+    prevX = readlane_u32(xv[15], 63);
+    uint32_t v[16];
+    uint32_t kw = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const uint32_t cur = xv[k];
-        uint32_t prv = dpp<kDppWaveShr1>(cur);
-        prv = (lane == 0) ? prevX : prv;
-        prevX = readlane_u32(cur, 63);
-        const uint32_t v = zz_enc16((uint16_t)(cur - prv));
-        const bool valid = Full || (t + 64u * (uint32_t)k + lane < n);
-        const bool nz = valid && v != 0, gt16 = v > 16, gt272 = v > 272;
-        const uint64_t bnz = ballot(nz), b16 = ballot(gt16), b272 = ballot(gt272);
-        const uint64_t b1 = bnz & ~b16, b2 = bnz & b16 & ~b272, b3 = bnz & b272;
-        if (nz && !gt16) W.S[fS + mbcnt(b1)] = (uint8_t)(v - 1u);
-        if (nz && gt16 && !gt272) W.M[fM + mbcnt(b2)] = (uint8_t)(v - 17u);
-        if (b3) {
-            if (nz && gt272) {
-                const uint32_t w = v - 273u, r = fL + mbcnt(b3);
-                W.L[r] = (uint8_t)w;
-                W.H[r] = (uint8_t)(w >> 8);
+    for (int m = 0; m < 16; m++) {
+        v[m] = zz_enc16((uint16_t)(xv[m] - prv));
+        prv = xv[m];
+        const bool valid = Full || (i0 + (uint32_t)m < n);
+        const uint32_t c = (valid && v[m] != 0) ? 1u + (v[m] > 16) + (v[m] > 272) : 0u;
+        kw |= c << (2 * m);
+    }
+    // places: step fills + the classes of the lanes below + my own running ranks
+    const uint32_t lo = kw & 0x55555555u, hi = (kw >> 1) & 0x55555555u;
+    const uint32_t n1 = (uint32_t)__builtin_popcount(lo & ~hi), n2 = (uint32_t)__builtin_popcount(hi & ~lo);
+    const uint32_t n3 = (uint32_t)__builtin_popcount(lo & hi);
+    const uint32_t p12 = n1 | (n2 << 16);
+    const uint32_t i12 = wave_incl_sum(p12), i3 = wave_incl_sum(n3);
+    const uint32_t t12 = readlane_u32(i12, 63), t3 = readlane_u32(i3, 63);
+    const uint32_t e12 = i12 - p12;
+    uint32_t qS = fS + (e12 & 0xFFFFu), qM = fM + (e12 >> 16), qL = fL + (i3 - n3);
+    const uint32_t dS = kDummy + 4u * lane;
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        const uint32_t c = (kw >> (2 * m)) & 3u;
+        W.S[c == 1 ? qS : dS] = (uint8_t)(v[m] - 1u);
+        W.M[c == 2 ? qM : dS] = (uint8_t)(v[m] - 17u);
+        qS += (c == 1);
+        qM += (c == 2);
+    }
+    if (t3) {
+#pragma unroll
+        for (int m = 0; m < 16; m++) {
+            const uint32_t c = (kw >> (2 * m)) & 3u;
+            if (c == 3) {
+                const uint32_t w = v[m] - 273u;
+                W.L[qL] = (uint8_t)w;
+                W.H[qL] = (uint8_t)(w >> 8);
+                qL++;
             }
         }
-        fS += (uint32_t)__builtin_popcountll(b1);
-        fM += (uint32_t)__builtin_popcountll(b2);
-        fL += (uint32_t)__builtin_popcountll(b3);
-        const uint32_t c = (uint32_t)nz + (uint32_t)(nz && gt16) + (uint32_t)(nz && gt272);
-        uint32_t kb = c << ksh;
-        kb |= dpp<kDppQuadSwap1>(kb);
-        kb |= dpp<kDppQuadSwap2>(kb);
-        W.K[16u * (uint32_t)k + (lane >> 2)] = (uint8_t)kb;
     }
+    fS += t12 & 0xFFFFu;
+    fM += t12 >> 16;
+    fL += t3;
+    return kw;
 }
 
 // sizes[5] = {keys, S, M, Llow, Lhigh} bytes.
@@ -137,14 +161,14 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
     uint32_t prevX = 0;                       // last sample of the previous sub-step (wave-uniform)
     for (uint32_t t = 0; t < n; t += kSplitStep) {
         const bool full = t + kSplitStep <= n;
-        if (full) split_step<true>(x, n, t, W, fS, fM, fL, prevX);
-        else split_step<false>(x, n, t, W, fS, fM, fL, prevX);
+        const uint32_t kw = full ? split_step<true>(x, n, t, W, fS, fM, fL, prevX)
+                                 : split_step<false>(x, n, t, W, fS, fM, fL, prevX);
         fH = fL;
-        lds_sync();
         const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
         uint8_t* kout = st.K + (t >> 2);
-        if (4u * lane + 4u <= nK) gst<uint32_t>(kout + 4u * lane, *(const uint32_t*)(W.K + 4u * lane));
-        else for (uint32_t b = 4u * lane; b < nK; b++) gst<uint8_t>(kout + b, W.K[b]);
+        if (4u * lane + 4u <= nK) gst<uint32_t>(kout + 4u * lane, kw);
+        else for (uint32_t b = 4u * lane; b < nK; b++) gst<uint8_t>(kout + b, (uint8_t)(kw >> (8u * (b - 4u * lane))));
+        lds_sync();
         nwin_flush(W.S, fS, st.S, gS);
         bwin_flush(W.M, fM, st.M, gM);
         bwin_flush(W.L, fL, st.Ll, gL);
@@ -173,14 +197,12 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
 // ---------------------------------------------------------------------------------------------
 // Merge over the reference's concatenated intermediate buffer (see oracle c5_merge): stream starts at
 // keys_length = ceil(n/4), then +dS, +dM, +dLl; a read past `total` is the reference's UB -> error.
-// Same lane mapping as the split (sub-step k gives lane l sample t + 64k + l).  Per step the class
-// counts come from the key bytes, the step's S/M/L bytes are staged into LDS with 16-byte loads,
-// each lane then reads its byte at the class fill plus its mbcnt rank, and the 16-bit delta sum is
-// a DPP wave scan.  `in` must stay readable 16 bytes past `total` (scratch padding).
+// Per 1024-sample step the class counts come from the key bytes, the step's S/M/L bytes are staged
+// into LDS with 16-byte loads, and each lane decodes 16 consecutive samples (merge_step).  `in`
+// must stay readable 16 bytes past `total` (scratch padding).
 // Returns 0 ok, 1 out-of-bounds; *consumed = one past the last Lhigh byte.
 // ---------------------------------------------------------------------------------------------
 struct MergeLds {
-    alignas(16) uint8_t K[kSplitStep / 4];
     alignas(16) uint8_t S[528];   // 513 bytes of nibbles + alignment
     alignas(16) uint8_t M[1040];  // 1024 + alignment
     alignas(16) uint8_t L[1040];
@@ -194,6 +216,49 @@ __device__ __forceinline__ uint64_t stage_bytes(uint8_t* W, const uint8_t* in, u
     const uint32_t nblk = (uint32_t)((a + len - a0 + 15) >> 4);
     for (uint32_t b = (uint32_t)lane_id(); b < nblk; b += 64) *(uint4*)(W + 16u * b) = gld<uint4>(in + a0 + 16u * b);
     return a0;
+}
+
+// Merge step over 1024 samples: lane l decodes the 16 consecutive samples t + 16l .. t + 16l + 15,
+// whose 16 keys are its own key word.  Its places in the S / M / L streams are the step's fills
+// plus the class counts of the lanes below it (one packed DPP scan), so each lane walks its 16
+// samples alone: one LDS byte read per stream and sample, a running 16-bit sum, and a second scan
+// carries the sum across lanes.  Outputs leave as two 16-byte stores per lane.
+template <bool Full>
+__device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, bool any3, uint32_t qS, uint32_t qM, uint32_t qL,
+                                           uint32_t dLH, uint32_t& carry, int16_t* __restrict__ out, uint32_t t,
+                                           uint32_t n)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t acc = 0;
+    uint32_t o[16];
+#pragma unroll
+    for (int m = 0; m < 16; m++) {
+        const uint32_t c = (kw >> (2 * m)) & 3u;
+        const uint32_t sb = ((uint32_t)W.S[qS >> 1] >> (4u * (qS & 1u))) & 15u;
+        const uint32_t mb = W.M[qM];
+        uint32_t v = (c == 1) ? sb + 1u : ((c == 2) ? mb + 17u : 0u);
+        if (any3 && c == 3) v = (((uint32_t)W.H[qL + dLH] << 8) | (uint32_t)W.L[qL]) + 273u;
+        qS += (c == 1);
+        qM += (c == 2);
+        qL += (c == 3);
+        acc += (uint32_t)zz_dec16((uint16_t)v);
+        o[m] = acc;
+    }
+    const uint32_t incl = wave_incl_sum(acc);
+    const uint32_t base = carry + incl - acc;
+    carry += readlane_u32(incl, 63);
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = ((o[2 * k] + base) & 0xFFFFu) | ((o[2 * k + 1] + base) << 16);
+    int16_t* dst = out + t + 16u * lane;
+    if (Full) {
+        gst<uint4>(dst, make_uint4(w[0], w[1], w[2], w[3]));
+        gst<uint4>(dst + 8, make_uint4(w[4], w[5], w[6], w[7]));
+    } else {
+#pragma unroll
+        for (int m = 0; m < 16; m++)
+            if (t + 16u * lane + (uint32_t)m < n) gst<uint16_t>(dst + m, (uint16_t)(w[m >> 1] >> (16 * (m & 1))));
+    }
 }
 
 __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
@@ -220,44 +285,32 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
             const uint32_t first = 16u * lane, nv = (n - t) > first ? (n - t) - first : 0u;
             if (nv < 16) kw &= (1u << (2u * nv)) - 1u;
         }
-        *(uint32_t*)(W.K + 4u * lane) = kw;
-        // class counts of the step
+        // class counts of my 16 samples, their lane prefix and the step totals
         const uint32_t lo = kw & 0x55555555u, hi = (kw >> 1) & 0x55555555u;
-        const uint32_t ns = wave_sum((uint32_t)__builtin_popcount(lo & ~hi));
-        const uint32_t nm = wave_sum((uint32_t)__builtin_popcount(hi & ~lo));
-        const uint32_t nl = wave_sum((uint32_t)__builtin_popcount(lo & hi));
+        const uint32_t n1 = (uint32_t)__builtin_popcount(lo & ~hi), n2 = (uint32_t)__builtin_popcount(hi & ~lo);
+        const uint32_t n3 = (uint32_t)__builtin_popcount(lo & hi);
+        const uint32_t p12 = n1 | (n2 << 16);
+        const uint32_t i12 = wave_incl_sum(p12), i3 = wave_incl_sum(n3);
+        const uint32_t t12 = readlane_u32(i12, 63);
+        const uint32_t ns = t12 & 0xFFFFu, nm = t12 >> 16, nl = readlane_u32(i3, 63);
         if (ps + ((sN + ns + 1) >> 1) > total || pm + mN + nm > total || pl + lN + nl > total || ph + lN + nl > total)
             return 1;
         const uint64_t wS = stage_bytes(W.S, in, ps + (sN >> 1), (uint32_t)(((sN + ns + 1) >> 1) - (sN >> 1)));
         const uint64_t wM = stage_bytes(W.M, in, pm + mN, nm);
-        const uint64_t wL = stage_bytes(W.L, in, pl + lN, nl);
-        const uint64_t wH = stage_bytes(W.H, in, ph + lN, nl);
-        lds_sync();
-        // window-relative fills: S in nibbles from the window start, M/L in bytes
-        uint32_t fS = (uint32_t)(2 * (ps - wS) + sN), fM = (uint32_t)(pm + mN - wM), fL = (uint32_t)(pl + lN - wL);
-        const uint32_t dLH = (uint32_t)((ph - wH) - (pl - wL));  // H window offset relative to L's
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const uint32_t i = t + 64u * (uint32_t)k + lane;
-            const uint32_t c = ((uint32_t)W.K[16u * (uint32_t)k + (lane >> 2)] >> (2u * (lane & 3u))) & 3u;
-            const uint64_t b1 = ballot(c == 1), b2 = ballot(c == 2), b3 = ballot(c == 3);
-            uint32_t v = 0;
-            if (c == 1) {
-                const uint32_t q = fS + mbcnt(b1);
-                v = (((uint32_t)W.S[q >> 1] >> (4u * (q & 1u))) & 15u) + 1u;
-            } else if (c == 2) {
-                v = (uint32_t)W.M[fM + mbcnt(b2)] + 17u;
-            } else if (c == 3) {
-                const uint32_t q = fL + mbcnt(b3);
-                v = (((uint32_t)W.H[q + dLH] << 8) | (uint32_t)W.L[q]) + 273u;
-            }
-            fS += (uint32_t)__builtin_popcountll(b1);
-            fM += (uint32_t)__builtin_popcountll(b2);
-            fL += (uint32_t)__builtin_popcountll(b3);
-            const uint32_t incl = wave_incl_sum(zz_dec16((uint16_t)v)) + carry;
-            carry = readlane_u32(incl, 63);
-            if (full || i < n) gst<uint16_t>(out + i, (uint16_t)incl);
+        uint64_t wL = 0, wH = 0;
+        if (nl) {
+            wL = stage_bytes(W.L, in, pl + lN, nl);
+            wH = stage_bytes(W.H, in, ph + lN, nl);
         }
+        lds_sync();
+        // window-relative places: S in nibbles from the window start, M/L in bytes
+        const uint32_t e12 = i12 - p12;
+        const uint32_t qS = (uint32_t)(2 * (ps - wS) + sN) + (e12 & 0xFFFFu);
+        const uint32_t qM = (uint32_t)(pm + mN - wM) + (e12 >> 16);
+        const uint32_t qL = (uint32_t)(pl + lN - wL) + (i3 - n3);
+        const uint32_t dLH = (uint32_t)((ph - wH) - (pl - wL));  // H window offset relative to L's
+        if (full) merge_step<true>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
+        else merge_step<false>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
         sN += ns;
         mN += nm;
         lN += nl;
