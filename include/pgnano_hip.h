@@ -92,6 +92,31 @@ int pgn_decompress_batch_device(pgn_ctx *ctx, size_t nchunks, const uint8_t *d_i
                                 const uint64_t *d_in_sizes, int16_t *d_samples, const uint64_t *d_sample_offsets,
                                 const uint32_t *d_sample_counts, int32_t *d_status, void *stream);
 
+/* ---- VBZ: the pod5 baseline codec (svb16 + zstd level 1), same context, same conventions ------
+ * pod5::compressed_signal_max_size (signal_compression.cpp:14-19):
+ * ZSTD_compressBound(svb16_max_encoded_length(n)) = ZSTD_compressBound(ceil(n/8) + 2n). */
+size_t pgn_vbz_compressed_signal_max_size(size_t sample_count);
+
+/* pod5::compress_signal(samples, pool, destination) (signal_compression.cpp:21-50): the compressed
+ * size in *out_size; a frame larger than dst_capacity is PGN_ERR_ZSTD_COMPRESS ("Failed to compress
+ * data").  Chunks whose svb16 buffer exceeds one zstd block (128 KiB) return PGN_ERR_UNSUPPORTED. */
+int pgn_vbz_compress_signal(pgn_ctx *ctx, const int16_t *samples, size_t sample_count, uint8_t *dst,
+                            size_t dst_capacity, size_t *out_size);
+
+/* pod5::decompress_signal(compressed, pool, destination) (signal_compression.cpp:96-141). */
+int pgn_vbz_decompress_signal(pgn_ctx *ctx, const uint8_t *compressed, size_t compressed_size, int16_t *dst,
+                              size_t sample_count);
+
+/* Batched device-resident VBZ encode / decode; arguments as pgn_compress_batch_device /
+ * pgn_decompress_batch_device (d_stats: svb16 bytes at [0], frame bytes at [5], others 0). */
+int pgn_vbz_compress_batch_device(pgn_ctx *ctx, size_t nchunks, const int16_t *d_samples,
+                                  const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts, uint8_t *d_out,
+                                  const uint64_t *d_out_offsets, const uint64_t *d_out_caps, uint64_t *d_out_sizes,
+                                  int32_t *d_status, uint64_t *d_stats, void *stream);
+int pgn_vbz_decompress_batch_device(pgn_ctx *ctx, size_t nchunks, const uint8_t *d_in, const uint64_t *d_in_offsets,
+                                    const uint64_t *d_in_sizes, int16_t *d_samples, const uint64_t *d_sample_offsets,
+                                    const uint32_t *d_sample_counts, int32_t *d_status, void *stream);
+
 /* Device generator of the synthetic nanopore-like reads used by bench.py (integer-only, identical
  * to the checker's pgno_synth_read): global read first_read + r * read_stride ->
  * d_samples[d_sample_offsets[r] .. + d_sample_counts[r]). */

@@ -415,29 +415,34 @@ int pgno_vbz_compress(const int16_t *x, uint32_t n, uint8_t *dst, size_t cap, si
 }
 
 /* pod5::decompress_signal (signal_compression.cpp:96-141) with svb16::decode_scalar
- * (svb16/decode_scalar.hpp).  The SSE path reads the same bytes; its 16-byte padding is part of
- * the intermediate allocation and drops out of the consumed check. */
+ * (svb16/decode_scalar.hpp).  The intermediate is the frame content plus svb16's 16 padding bytes
+ * (signal_compression.cpp:111-118; decode.hpp:16-23 on x86-64): ZSTD_decompress gets that whole
+ * capacity, and "consumed + padding == size" makes any read into the padding the "Remaining data"
+ * error.  Reads past the padding are out of bounds in the reference: PGNO_ERR_CORRUPT here.  The
+ * SSE path reads the same bytes (it consumes exactly what the scalar decoder consumes). */
+#define VBZ_PADDING 16u
 int pgno_vbz_decompress(const uint8_t *src, size_t len, int16_t *out, uint32_t n)
 {
     if (!zok()) return PGNO_ERR_NO_ZSTD;
     unsigned long long cs = Z.fcs(src, len);
     if (Z.iserror((size_t)cs)) return PGNO_ERR_NOT_ZSTD;
-    uint8_t *inter = (uint8_t *)malloc(cs ? cs : 1);
+    size_t total = (size_t)cs + VBZ_PADDING;
+    uint8_t *inter = (uint8_t *)calloc(total, 1);
     if (!inter) return PGNO_ERR_ALLOC;
-    size_t r = Z.decompress(inter, (size_t)cs, src, len);
+    size_t r = Z.decompress(inter, total, src, len);
     if (Z.iserror(r)) { free(inter); return PGNO_ERR_ZSTD_DECOMPRESS; }
     size_t nk = ((size_t)n >> 3) + ((((size_t)n & 7u) + 7u) >> 3);
+    if (nk > cs) { free(inter); return nk <= total ? PGNO_ERR_REMAINING : PGNO_ERR_CORRUPT; }
     size_t p = nk;
     uint16_t prev = 0;
     for (uint32_t i = 0; i < n; i++) {
-        if ((i >> 3) >= cs) { free(inter); return PGNO_ERR_CORRUPT; }
         unsigned big = (inter[i >> 3] >> (i & 7u)) & 1u;
         uint16_t v;
         if (!big) {
-            if (p >= cs) { free(inter); return PGNO_ERR_CORRUPT; }
+            if (p >= total) { free(inter); return PGNO_ERR_CORRUPT; }
             v = inter[p++];
         } else {
-            if (p + 1 >= cs) { free(inter); return PGNO_ERR_CORRUPT; }
+            if (p + 1 >= total) { free(inter); return PGNO_ERR_CORRUPT; }
             v = (uint16_t)(inter[p] | ((uint16_t)inter[p + 1] << 8));
             p += 2;
         }

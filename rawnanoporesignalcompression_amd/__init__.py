@@ -1,4 +1,4 @@
-"""MI355X-native pgnano (C5) raw nanopore signal codec.
+"""MI355X-native pgnano (C5) and VBZ raw nanopore signal codecs.
 
 Drop-in for the reference's pgnano plugin surface (pgnano::compress_signal /
 pgnano::decompress_signal); the work runs in hand-written gfx950 kernels behind the C ABI in
@@ -9,11 +9,13 @@ from .codec import (
     EncodedBatch,
     PGNanoCodec,
     PGNanoError,
+    VBZCodec,
     compress_signal,
     compressed_signal_max_size,
     decompress_signal,
     default_codec,
     pinanoraw_compress_signal,
+    vbz_compressed_signal_max_size,
 )
 
 __all__ = [
@@ -22,10 +24,12 @@ __all__ = [
     "PGN_MAX_CHUNK_SAMPLES",
     "PGNanoCodec",
     "PGNanoError",
+    "VBZCodec",
     "compress_signal",
     "compressed_signal_max_size",
     "decompress_signal",
     "default_codec",
     "load_native",
     "pinanoraw_compress_signal",
+    "vbz_compressed_signal_max_size",
 ]

@@ -9,6 +9,9 @@ Reference interface (tomas-gr/RawNanoporeSignalCompression):
 * ``pgnano::decompress_signal(compressed, pool, destination, state) -> Status``
   (pgnano.h:13-17, pgnano.cpp:98-126 -> C5.hpp:477-683).
 * ``pod5_pinanoraw_compress_signal`` (c_api.cpp:1217-1253).
+* the pod5 baseline codec VBZ, ``pod5::compress_signal`` / ``pod5::decompress_signal`` /
+  ``pod5::compressed_signal_max_size`` (pod5/c++/pod5_format/signal_compression.cpp:14-141), as
+  :class:`VBZCodec` with the same methods (the ``--VBZ`` side of the reference's copy tool).
 
 ``read_data`` / ``is_last_batch`` / ``state`` are accepted and ignored, exactly as C5 ignores them.
 Errors raise :class:`PGNanoError` carrying the reference's status message.
@@ -69,6 +72,20 @@ class EncodedBatch:
 class PGNanoCodec:
     """One codec context per HIP device (one process per GPU)."""
 
+    # C-ABI entry points of this codec
+    _fn_compress, _fn_decompress = "pgn_compress_signal", "pgn_decompress_signal"
+    _fn_compress_batch, _fn_decompress_batch = "pgn_compress_batch_device", "pgn_decompress_batch_device"
+
+    @staticmethod
+    def max_size(sample_count: int) -> int:
+        return compressed_signal_max_size(sample_count)
+
+    @staticmethod
+    def _default_caps(counts):
+        import torch
+
+        return torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
+
     def __init__(self, device: int = 0):
         self._lib = _native.load()
         h = C.c_void_p()
@@ -94,10 +111,11 @@ class PGNanoCodec:
     # ---- per-chunk plugin surface (host memory) -------------------------------------------
     def compress_signal(self, samples, read_data=None, is_last_batch: bool = False) -> bytes:
         x = np.ascontiguousarray(samples, dtype=np.int16)
-        cap = compressed_signal_max_size(x.size)
+        cap = self.max_size(x.size)
         out = np.empty(cap, dtype=np.uint8)
         size = C.c_size_t(0)
-        rc = self._lib.pgn_compress_signal(self._h, x.ctypes.data, x.size, out.ctypes.data, cap, C.byref(size))
+        rc = getattr(self._lib, self._fn_compress)(self._h, x.ctypes.data, x.size, out.ctypes.data, cap,
+                                                   C.byref(size))
         if rc == _native.PGN_ERR_DST_TOO_SMALL:
             raise PGNanoError(rc, f"Destination size: {cap}, Required size: {size.value}")
         _check(rc)
@@ -111,8 +129,8 @@ class PGNanoCodec:
             destination = np.empty(int(sample_count), dtype=np.int16)
         if destination.dtype != np.int16 or not destination.flags.c_contiguous:
             raise ValueError("destination must be a contiguous int16 array")
-        _check(self._lib.pgn_decompress_signal(self._h, src.ctypes.data if src.size else 0, src.size,
-                                               destination.ctypes.data, destination.size))
+        _check(getattr(self._lib, self._fn_decompress)(self._h, src.ctypes.data if src.size else 0, src.size,
+                                                       destination.ctypes.data, destination.size))
         return destination
 
     # ---- batched device API -----------------------------------------------------------------
@@ -130,7 +148,7 @@ class PGNanoCodec:
         counts = sample_counts.to(device=dev, dtype=torch.int32).contiguous()
         offs = sample_offsets.to(device=dev, dtype=torch.int64).contiguous()
         if out_caps is None:
-            caps = torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
+            caps = self._default_caps(counts)
         else:
             caps = out_caps.to(device=dev, dtype=torch.int64).contiguous()
         if out_offsets is None:
@@ -145,7 +163,7 @@ class PGNanoCodec:
         sizes = torch.zeros(n, dtype=torch.int64, device=dev)
         status = torch.full((n,), -1, dtype=torch.int32, device=dev)
         stats = torch.zeros((n, _native.PGN_STATS_PER_CHUNK), dtype=torch.int64, device=dev) if with_stats else None
-        _check(self._lib.pgn_compress_batch_device(
+        _check(getattr(self._lib, self._fn_compress_batch)(
             self._h, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
             _ptr(status), _ptr(stats), stream or 0))
         return EncodedBatch(out, oo, caps, sizes, status, stats)
@@ -168,7 +186,7 @@ class PGNanoCodec:
             total = int(counts.to(torch.int64).sum().item())
             out = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
         status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-        _check(self._lib.pgn_decompress_batch_device(
+        _check(getattr(self._lib, self._fn_decompress_batch)(
             self._h, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
             _ptr(blob_sizes.to(torch.int64).contiguous()), _ptr(out), _ptr(so), _ptr(counts), _ptr(status),
             stream or 0))
@@ -200,6 +218,33 @@ class PGNanoCodec:
 
     def last_decode_ms(self) -> float:
         return float(self._lib.pgn_ctx_last_decode_ms(self._h))
+
+
+def vbz_compressed_signal_max_size(sample_count: int) -> int:
+    """``pod5::compressed_signal_max_size`` (signal_compression.cpp:14-19)."""
+    return int(_native.load().pgn_vbz_compressed_signal_max_size(sample_count))
+
+
+class VBZCodec(PGNanoCodec):
+    """The pod5 VBZ codec (svb16 + zstd level 1) on the GPU: ``pod5::compress_signal`` /
+    ``pod5::decompress_signal`` (signal_compression.cpp:21-141), same methods as
+    :class:`PGNanoCodec`.  A frame larger than the destination raises "Failed to compress data"."""
+
+    _fn_compress, _fn_decompress = "pgn_vbz_compress_signal", "pgn_vbz_decompress_signal"
+    _fn_compress_batch, _fn_decompress_batch = "pgn_vbz_compress_batch_device", "pgn_vbz_decompress_batch_device"
+
+    @staticmethod
+    def max_size(sample_count: int) -> int:
+        return vbz_compressed_signal_max_size(sample_count)
+
+    @staticmethod
+    def _default_caps(counts):
+        import torch
+
+        c = counts.to(torch.int64)
+        svb = (c >> 3) + (((c & 7) + 7) >> 3) + 2 * c
+        small = (svb < 128 * 1024).to(torch.int64)
+        return svb + (svb >> 8) + small * ((128 * 1024 - svb).clamp(min=0) >> 11)
 
 
 _default: PGNanoCodec | None = None

@@ -13,6 +13,7 @@
 
 #include "../../include/pgnano_hip.h"
 #include "pgn_c5.h"
+#include "pgn_vbz.h"
 #include "pgn_zdec.h"
 #include "pgn_zenc.h"
 
@@ -23,6 +24,9 @@ constexpr uint32_t kMaxStream = kMaxSamples;            // largest C5 stream (M/
 constexpr uint32_t kMaxEncSeq = kMaxStream / 4 + 2;      // every match covers >= 4 bytes
 constexpr uint32_t kMaxDecSeq = kMaxStream / 3 + 2;      // any valid block: matches >= 3 bytes
 constexpr int kStreams = 5;
+// Codecs of a batch call: the pgnano C5 variant (5 zstd frames per chunk) and the pod5 VBZ codec
+// (one zstd frame per chunk).  Both share the per-chunk buffers and the zstd kernels.
+enum Codec : int { kCodecC5 = 0, kCodecVbz = 1 };
 
 __host__ __device__ constexpr size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -93,6 +97,9 @@ __host__ __device__ inline DecLayout dec_layout()
     return l;
 }
 constexpr size_t kInterCap = (size_t)5 * kMaxStream;
+// svb16::decode_input_buffer_padding_byte_count() on x86-64 (svb16/decode.hpp:16-23): the VBZ
+// intermediate is the frame content plus 16 bytes, and ZSTD_decompress may fill them.
+constexpr size_t kVbzPadding = 16;
 constexpr size_t kChunkInterBytes = align_up(kInterCap + 64, 256);
 
 // Work-unit order of the per-stream kernels: the large streams first (M, S, keys, Llow, Lhigh), so
@@ -123,6 +130,7 @@ struct EncArgs {
     uint32_t* queue;     // work counter of this sub-batch
     uint64_t* prof;
     size_t base, G;
+    uint32_t nu;         // zstd work units per chunk: 5 (C5) or 1 (VBZ)
 };
 
 __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
@@ -169,13 +177,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
     uint32_t epoch = a.epochs[blockIdx.x];
     PhaseProf P;
     P.init(a.prof);
-    const size_t G = a.G, units = kStreams * G;
+    const size_t G = a.G, units = (size_t)a.nu * G;
     while (true) {
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(a.queue, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= units) break;
-        const int s = unit_stream((uint32_t)(u / G));
+        const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
         const size_t g = u % G;
         if (a.base + g >= a.nchunks) continue;
         const uint32_t n = a.sizes[g * kStreams + s];
@@ -185,7 +193,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
             epoch = 1;
             wave_sync();
         }
-        const uint8_t* src = a.streams + g * kChunkStreamBytes + stream_off(s);
+        // VBZ: the svb16 buffer starts at the offset its split recorded in sizes[1]
+        const uint8_t* src = a.streams + g * kChunkStreamBytes + (a.nu == 1 ? a.sizes[g * kStreams + 1] : stream_off(s));
         uint8_t* dst = a.frames + g * kChunkFrameBytes + frame_off(s);
         const size_t fsz = zstd1_compress_wave(dst, src, n, S, epoch, P);
         if (lane == 0) a.fsizes[g * kStreams + s] = (uint32_t)fsz;
@@ -267,6 +276,7 @@ struct DecArgs {
     uint32_t* queue;
     uint64_t* prof;
     size_t base, G;
+    uint32_t nu;         // zstd work units per chunk: 5 (C5) or 1 (VBZ)
 };
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
@@ -325,18 +335,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.xch = (uint32_t*)(sbase + lay.xch);
     PhaseProf P;
     P.init(a.prof);
-    const size_t G = a.G, units = kStreams * G;
+    const size_t G = a.G, units = (size_t)a.nu * G;
     while (true) {
         uint32_t u = 0;
         if (lane == 0) u = atomicAdd(a.queue, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= units) break;
-        const int s = unit_stream((uint32_t)(u / G));
+        const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
         const size_t g = u % G;
         const size_t c = a.base + g;
         if (c >= a.nchunks || a.status[c] != PGN_OK) continue;
         DecUnit& d = a.units[g * kStreams + s];
-        const long r = zstd_decompress_wave(a.in + d.src, d.len, a.inter + g * kChunkInterBytes + d.interOff, d.cs, S, P);
+        // destination capacity: the frame content size (C5.hpp:588-667 sizes each stream's slot
+        // exactly); VBZ's intermediate carries svb16's 16 padding bytes (signal_compression.cpp:112-118)
+        const size_t cap = a.nu == 1 ? (size_t)d.cs + kVbzPadding : (size_t)d.cs;
+        const long r = zstd_decompress_wave(a.in + d.src, d.len, a.inter + g * kChunkInterBytes + d.interOff, cap, S, P);
         if (lane == 0) d.dres = (int32_t)r;
         wave_sync();
     }
@@ -364,6 +377,126 @@ __global__ __launch_bounds__(64) void dec_merge_kernel(DecArgs a)
                                       (uint64_t)d[3].dres, a.samples + a.sampleOffsets[c], a.sampleCounts[c], &consumed);
         if (bad) st = PGN_ERR_CORRUPT;
         else if (consumed != total) st = PGN_ERR_REMAINING;
+    }
+    if (lane_id() == 0) a.status[c] = st;
+    P.mark(6);
+    P.flush();
+}
+
+// ---------------------------------------------------------------------------------------------
+// VBZ (pod5::compress_signal / decompress_signal, signal_compression.cpp:37-141): split -> one
+// zstd frame per chunk -> copy into place; parse -> zstd decode -> svb16 merge.  The per-chunk
+// buffers are the C5 ones (a chunk's stream area holds its svb16 buffer, <= 2.125 n bytes).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void vbz_split_kernel(EncArgs a)
+{
+    static __shared__ VbzSplitLds W;
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    PhaseProf P;
+    P.init(a.prof);
+    const uint32_t n = a.sampleCounts[c];
+    uint32_t* sz = a.sizes + g * kStreams;
+    if (n > kMaxSamples) {
+        if (lane_id() == 0) {
+            sz[0] = ~0u;
+            a.status[c] = PGN_ERR_UNSUPPORTED;
+            a.outSizes[c] = 0;
+        }
+        return;
+    }
+    // place the buffer so that its data part (after the ceil(n/8) key bytes) is 16-byte aligned
+    const uint32_t pad = (16u - (svb_key_length(n) & 15u)) & 15u;
+    const uint32_t m = vbz_split_wave(a.samples + a.sampleOffsets[c], n, a.streams + g * kChunkStreamBytes + pad, W);
+    if (lane_id() == 0) {
+        if (m > z1::kMaxSrc) {  // more than one zstd block: not on the GPU path yet
+            sz[0] = ~0u;
+            a.status[c] = PGN_ERR_UNSUPPORTED;
+            a.outSizes[c] = 0;
+        } else {
+            sz[0] = m;
+            sz[1] = pad;
+        }
+    }
+    P.mark(0);
+    P.flush();
+}
+
+__global__ __launch_bounds__(64) void vbz_assemble_kernel(EncArgs a)
+{
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    const int lane = lane_id();
+    const uint32_t* sz = a.sizes + g * kStreams;
+    if (sz[0] == ~0u) return;
+    const uint32_t fs = a.fsizes[g * kStreams];
+    // ZSTD_compress into the caller's span fails when the frame does not fit
+    // (signal_compression.cpp:57-62 "Failed to compress data")
+    const bool ok = fs <= a.outCaps[c];
+    if (ok) wave_copy(a.out + a.outOffsets[c], a.frames + g * kChunkFrameBytes, fs);
+    if (lane == 0) {
+        a.status[c] = ok ? PGN_OK : PGN_ERR_ZSTD_COMPRESS;
+        a.outSizes[c] = ok ? fs : 0;
+        if (a.stats) {
+            for (int s = 0; s < PGN_STATS_PER_CHUNK; s++) a.stats[c * PGN_STATS_PER_CHUNK + s] = 0;
+            a.stats[c * PGN_STATS_PER_CHUNK] = sz[0];
+            a.stats[c * PGN_STATS_PER_CHUNK + 5] = fs;
+        }
+    }
+}
+
+// one thread per chunk: ZSTD_getFrameContentSize (signal_compression.cpp:100-109)
+__global__ __launch_bounds__(64) void vbz_parse_kernel(DecArgs a)
+{
+    const size_t g = (size_t)blockIdx.x * 64 + lane_id();
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    DecUnit* u = a.units + g * kStreams;
+    bool ok = false;
+    const uint64_t src0 = a.inOffsets[c], len = a.inSizes[c];
+    const uint64_t cs = z1::frame_content_size(a.in + src0, (size_t)len, &ok);
+    int st = PGN_OK;
+    if (!ok) st = PGN_ERR_NOT_ZSTD;
+    else if (cs + kVbzPadding > kInterCap || len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
+    else {
+        u->src = src0;
+        u->len = (uint32_t)len;
+        u->cs = (uint32_t)cs;
+        u->interOff = 0;
+        u->dres = 0;
+    }
+    a.status[c] = st;
+}
+
+__global__ __launch_bounds__(64) void vbz_merge_kernel(DecArgs a)
+{
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    if (a.status[c] != PGN_OK) return;
+    PhaseProf P;
+    P.init(a.prof);
+    const DecUnit* d = a.units + g * kStreams;
+    int st = PGN_OK;
+    if (d->dres < 0) {
+        st = PGN_ERR_ZSTD_DECOMPRESS;
+    } else {
+        // svb16::decode over the padded intermediate, then "consumed + padding == size"
+        // (signal_compression.cpp:124-131): bytes past the content but inside the padding are the
+        // "Remaining data" error, beyond it the reference reads out of bounds
+        uint64_t consumed = 0;
+        const uint32_t n = a.sampleCounts[c];
+        const uint64_t total = (uint64_t)d->cs + kVbzPadding;
+        if (svb_key_length(n) > d->cs) {  // keys alone run into the padding (or past it)
+            st = svb_key_length(n) <= total ? PGN_ERR_REMAINING : PGN_ERR_CORRUPT;
+        } else {
+            const int bad = vbz_merge_wave(a.inter + g * kChunkInterBytes, total, a.samples + a.sampleOffsets[c], n,
+                                           &consumed);
+            if (bad) st = PGN_ERR_CORRUPT;
+            else if (consumed != d->cs) st = PGN_ERR_REMAINING;
+        }
     }
     if (lane_id() == 0) a.status[c] = st;
     P.mark(6);
@@ -639,7 +772,7 @@ static int ensure_queues(pgn_ctx* c, size_t n, hipStream_t s)
     return PGN_OK;
 }
 
-static int launch_encode(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
+static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
                          const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
                          const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
                          void* stream)
@@ -648,7 +781,8 @@ static int launch_encode(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, c
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
     const size_t passes = (nchunks + G - 1) / G;
-    const size_t slots = kStreams * G < c->encSlotsMax ? kStreams * G : c->encSlotsMax;
+    const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
+    const size_t slots = nu * G < c->encSlotsMax ? nu * G : c->encSlotsMax;
     int rc = ensure_enc(c, slots, G);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[0], s));
@@ -674,12 +808,19 @@ static int launch_encode(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, c
     a.epochs = c->epochs;
     a.prof = c->prof;
     a.G = G;
+    a.nu = nu;
     for (size_t p = 0; p < passes; p++) {
         a.base = p * G;
         a.queue = c->queues + p;
-        hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        if (codec == kCodecVbz) {
+            hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(vbz_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        }
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
@@ -687,7 +828,7 @@ static int launch_encode(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, c
     return PGN_OK;
 }
 
-static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
+static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
                          const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
                          const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
 {
@@ -695,7 +836,8 @@ static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const 
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
     const size_t passes = (nchunks + G - 1) / G;
-    const size_t slots = kStreams * G < c->decSlotsMax ? kStreams * G : c->decSlotsMax;
+    const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
+    const size_t slots = nu * G < c->decSlotsMax ? nu * G : c->decSlotsMax;
     int rc = ensure_dec(c, slots, G);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[2], s));
@@ -717,12 +859,19 @@ static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const 
     a.slotBytes = dec_layout().bytes;
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.G = G;
+    a.nu = nu;
     for (size_t p = 0; p < passes; p++) {
         a.base = p * G;
         a.queue = c->queues + p;
-        hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        if (codec == kCodecVbz) {
+            hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        }
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], s));
@@ -730,30 +879,64 @@ static int launch_decode(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const 
     return PGN_OK;
 }
 
-int pgn_compress_batch_device(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
-                              const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
-                              const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
-                              void* stream)
+static int compress_batch(int codec, pgn_ctx* c, size_t nchunks, const int16_t* d_samples,
+                          const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, uint8_t* d_out,
+                          const uint64_t* d_out_offsets, const uint64_t* d_out_caps, uint64_t* d_out_sizes,
+                          int32_t* d_status, uint64_t* d_stats, void* stream)
 {
     if (!c || !d_samples || !d_sample_offsets || !d_sample_counts || !d_out || !d_out_offsets || !d_out_caps ||
         !d_out_sizes || !d_status)
         return PGN_ERR_INVALID_ARG;
     if (nchunks == 0) return PGN_OK;
     std::lock_guard<std::mutex> g(c->mu);
-    return launch_encode(c, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets, d_out_caps,
+    return launch_encode(c, codec, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets, d_out_caps,
                          d_out_sizes, d_status, d_stats, stream);
+}
+
+static int decompress_batch(int codec, pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                            const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
+                            const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
+{
+    if (!c || !d_in || !d_in_offsets || !d_in_sizes || !d_samples || !d_sample_offsets || !d_sample_counts || !d_status)
+        return PGN_ERR_INVALID_ARG;
+    if (nchunks == 0) return PGN_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    return launch_decode(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets, d_sample_counts,
+                         d_status, stream);
+}
+
+int pgn_compress_batch_device(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
+                              const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
+                              const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
+                              void* stream)
+{
+    return compress_batch(kCodecC5, c, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
+                          d_out_caps, d_out_sizes, d_status, d_stats, stream);
 }
 
 int pgn_decompress_batch_device(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
                                 const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
                                 const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
 {
-    if (!c || !d_in || !d_in_offsets || !d_in_sizes || !d_samples || !d_sample_offsets || !d_sample_counts || !d_status)
-        return PGN_ERR_INVALID_ARG;
-    if (nchunks == 0) return PGN_OK;
-    std::lock_guard<std::mutex> g(c->mu);
-    return launch_decode(c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets, d_sample_counts,
-                         d_status, stream);
+    return decompress_batch(kCodecC5, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                            d_sample_counts, d_status, stream);
+}
+
+int pgn_vbz_compress_batch_device(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
+                                  const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
+                                  const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status,
+                                  uint64_t* d_stats, void* stream)
+{
+    return compress_batch(kCodecVbz, c, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
+                          d_out_caps, d_out_sizes, d_status, d_stats, stream);
+}
+
+int pgn_vbz_decompress_batch_device(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                                    const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
+                                    const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
+{
+    return decompress_batch(kCodecVbz, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                            d_sample_counts, d_status, stream);
 }
 
 int pgn_debug_phase_cycles(pgn_ctx* c, uint64_t* out, int n)
@@ -851,7 +1034,8 @@ struct StageHdr {
     uint64_t stats[PGN_STATS_PER_CHUNK];
 };
 
-int pgn_compress_signal(pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap, size_t* out_size)
+static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap,
+                           size_t* out_size)
 {
     if (!c || (!samples && n) || !dst || !out_size) return PGN_ERR_INVALID_ARG;
     if (n > kMaxSamples) return PGN_ERR_UNSUPPORTED;
@@ -871,7 +1055,7 @@ int pgn_compress_signal(pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* d
     HIPCHK(hipMemcpyAsync(dh, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
     if (n) HIPCHK(hipMemcpyAsync(din, samples, 2 * n, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
-    rc = launch_encode(c, 1, (const int16_t*)din, &d->off0, &d->count, dout, &d->outOff, &d->outCap,
+    rc = launch_encode(c, codec, 1, (const int16_t*)din, &d->off0, &d->count, dout, &d->outOff, &d->outCap,
                                    &d->outSize, &d->status, d->stats, c->stream);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(&h, dh, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -882,7 +1066,7 @@ int pgn_compress_signal(pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* d
     return PGN_OK;
 }
 
-int pgn_decompress_signal(pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
+static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
 {
     if (!c || (!src && len) || (!dst && n)) return PGN_ERR_INVALID_ARG;
     if (n > kMaxSamples) return PGN_ERR_UNSUPPORTED;
@@ -902,7 +1086,7 @@ int pgn_decompress_signal(pgn_ctx* c, const uint8_t* src, size_t len, int16_t* d
     HIPCHK(hipMemcpyAsync(dh, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
     if (len) HIPCHK(hipMemcpyAsync(din, src, len, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
-    rc = launch_decode(c, 1, din, &d->inOff, &d->inSize, dout, &d->off0, &d->count, &d->status,
+    rc = launch_decode(c, codec, 1, din, &d->inOff, &d->inSize, dout, &d->off0, &d->count, &d->status,
                                          c->stream);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(&h, dh, sizeof(h), hipMemcpyDeviceToHost, c->stream));
@@ -910,6 +1094,31 @@ int pgn_decompress_signal(pgn_ctx* c, const uint8_t* src, size_t len, int16_t* d
     if (h.status != PGN_OK) return h.status;
     if (n) HIPCHK(hipMemcpy(dst, dout, 2 * n, hipMemcpyDeviceToHost));
     return PGN_OK;
+}
+
+int pgn_compress_signal(pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap, size_t* out_size)
+{
+    return compress_signal(kCodecC5, c, samples, n, dst, cap, out_size);
+}
+
+int pgn_decompress_signal(pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
+{
+    return decompress_signal(kCodecC5, c, src, len, dst, n);
+}
+
+size_t pgn_vbz_compressed_signal_max_size(size_t n)
+{
+    return z1::compress_bound((size_t)svb_key_length((uint32_t)n) + 2 * n);
+}
+
+int pgn_vbz_compress_signal(pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap, size_t* out_size)
+{
+    return compress_signal(kCodecVbz, c, samples, n, dst, cap, out_size);
+}
+
+int pgn_vbz_decompress_signal(pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
+{
+    return decompress_signal(kCodecVbz, c, src, len, dst, n);
 }
 
 static pgn_ctx* g_default = nullptr;

@@ -42,6 +42,8 @@ def oracle() -> C.CDLL:
         L.pgno_c5_split.argtypes = [C.c_void_p, C.c_uint32] + [C.c_void_p] * 6
         L.pgno_vbz_compress.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t)]
         L.pgno_vbz_decompress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32]
+        L.pgno_vbz_svb_encode.restype = C.c_size_t
+        L.pgno_vbz_svb_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         L.pgno_vbz_bound.restype = C.c_size_t
         L.pgno_vbz_bound.argtypes = [C.c_uint32]
         L.pgno_synth_read.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint32, C.c_int32,
