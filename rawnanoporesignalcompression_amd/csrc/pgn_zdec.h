@@ -562,6 +562,20 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     int32_t q = S;
     uint32_t stored = 0, npend = 0;  // symbols stored to the slice / held in pend
     uint64_t pend = 0;
+    // full dwords wait in a 16-byte accumulator and leave as one aligned 16-byte store: a lane's
+    // slice line is then written in 8 whole pieces instead of 32 (fewer partially dirty L2 lines)
+    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, na = 0;
+    auto push = [&](uint32_t w) {
+        a0 = na == 0 ? w : a0;
+        a1 = na == 1 ? w : a1;
+        a2 = na == 2 ? w : a2;
+        a3 = na == 3 ? w : a3;
+        if (++na == 4) {
+            if (stored + 16 <= kSliceCap) gst<uint4>(slice + stored, make_uint4(a0, a1, a2, a3));
+            stored += 16;
+            na = 0;
+        }
+    };
     {
         const int32_t rounds = (int32_t)wave_max((uint32_t)((S - E + kRoundBits - 1) / kRoundBits));
         uint4 nx[5];
@@ -599,10 +613,9 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             };
             auto flush4 = [&]() {
                 if (npend >= 4) {
-                    if (stored + 4 <= kSliceCap) gst<uint32_t>(slice + stored, (uint32_t)pend);
+                    push((uint32_t)pend);
                     pend >>= 32;
                     npend -= 4;
-                    stored += 4;
                 }
             };
             // the first kBmpBits bits below S: record every codeword boundary for the walk
@@ -631,9 +644,8 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                     }
                 }
                 pend |= (uint64_t)word << (8 * npend);
-                if (stored + 4 <= kSliceCap) gst<uint32_t>(slice + stored, (uint32_t)pend);
+                push((uint32_t)pend);
                 pend >>= 32;
-                stored += 4;
             }
             while (ballot(q > lo)) {
 #pragma unroll
@@ -641,6 +653,12 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 flush4();
             }
             lds_sync();
+        }
+        // the accumulator's dwords, then the pending bytes
+        for (uint32_t t = 0; t < na; t++) {
+            const uint32_t w = t == 0 ? a0 : (t == 1 ? a1 : a2);
+            if (stored + 4 <= kSliceCap) gst<uint32_t>(slice + stored, w);
+            stored += 4;
         }
         for (uint32_t t = 0; t < npend; t++)
             if (stored + t < kSliceCap) gst<uint8_t>(slice + stored + t, (uint8_t)(pend >> (8 * t)));
