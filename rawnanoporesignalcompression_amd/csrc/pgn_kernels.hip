@@ -80,7 +80,7 @@ __host__ __device__ inline EncLayout enc_layout()
 }
 
 struct DecLayout {
-    size_t lit, htmp, seqs, tables, htab, xch, bytes;
+    size_t lit, seqs, tables, htab, bytes;
 };
 __host__ __device__ inline DecLayout dec_layout()
 {
@@ -88,11 +88,9 @@ __host__ __device__ inline DecLayout dec_layout()
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o = align_up(o + n + 64, 256); return r; };
     l.lit = take(kMaxStream);
-    l.htmp = take((size_t)64 * kSliceCap);
     l.seqs = take(12 * (size_t)kMaxDecSeq);
     l.tables = take(4 * ((size_t)kSeqTab + 4));
     l.htab = take(2u << z1::kHufTableLogMax);
-    l.xch = take(4 * 8 * 64);
     l.bytes = o;
     return l;
 }
@@ -327,12 +325,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
     DecScratch S;
     S.lit = sbase + lay.lit;
-    S.htmp = sbase + lay.htmp;
     S.seqs = (uint32_t*)(sbase + lay.seqs);
     S.maxSeq = kMaxDecSeq;
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
-    S.xch = (uint32_t*)(sbase + lay.xch);
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = (size_t)a.nu * G;
@@ -938,6 +934,21 @@ int pgn_vbz_decompress_batch_device(pgn_ctx* c, size_t nchunks, const uint8_t* d
     return decompress_batch(kCodecVbz, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                             d_sample_counts, d_status, stream);
 }
+
+#ifdef PGN_DEBUG_HUF
+// diagnostic build only: the Huffman decoder's record buffer (count, then records of 8 words)
+int pgn_debug_huf_dump(uint32_t* out, size_t nwords)
+{
+    uint32_t cnt = 0;
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(gHufDbgN), 4));
+    out[0] = cnt;
+    size_t m = cnt < (1u << 18) ? cnt : (1u << 18);
+    if (m > nwords - 1) m = nwords - 1;
+    HIPCHK(hipMemcpyFromSymbol(out + 1, HIP_SYMBOL(gHufDbg), 4 * m));
+    return PGN_OK;
+}
+#endif
 
 int pgn_debug_phase_cycles(pgn_ctx* c, uint64_t* out, int n)
 {

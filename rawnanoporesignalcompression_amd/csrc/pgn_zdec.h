@@ -9,12 +9,9 @@
 
 namespace pgn {
 
-constexpr int kBmpBits = 256;            // speculative boundaries recorded per lane: bit d = position S - d
-constexpr int32_t kRoundBits = 512;      // phase-1 bits per round
-constexpr int kStgWords = 20;            // staged bytes per lane per round: 80 >= (512 + 16 + 31) / 8 + 8
-constexpr uint32_t kSliceCap = 8192;     // speculative symbols kept per lane (htmp slice)
-constexpr int kBnd = 24;                 // stream bytes [S/8 - 20, S/8 + 4) cached per lane for the walk
-constexpr int kBndBelow = 20;
+constexpr int32_t kWinBits = 256;        // Huffman stream bits per lane per round (pgn_huf4.h)
+constexpr int kBmpBits = 128;            // speculative boundaries recorded per lane: bit d = position hi - d
+constexpr int kStgWords = 12;            // staged bytes per lane per round: 48 >= (256 + 63) / 8 + 8
 
 constexpr int kSeqWin = 2048;            // sequences bitstream window staged in LDS
 constexpr int kSeqHdr = 400;             // staged sequences-section header (table descriptions)
@@ -57,12 +54,10 @@ static __shared__ DecLds sDec;
 
 struct DecScratch {
     uint8_t* lit;           // literals of a block with sequences (<= 128 KiB)
-    uint8_t* htmp;          // 64 * kSliceCap speculative Huffman symbols
     uint32_t* seqs;         // decoded sequences: {litLength, matchLength, offset} triples
     uint32_t maxSeq;
     uint32_t* tables;       // the three sequence FSE tables of a multi-block frame (kSeqTab + 4 words)
     uint16_t* htab;         // 4096 entries: a 12-bit Huffman table, or the parked LDS table
-    uint32_t* xch;          // 8 x 64 words: per-lane values of the serial border walk (rare path)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -105,8 +100,7 @@ __device__ __forceinline__ uint32_t rb_huf(RevBits& r, int32_t& pos, unsigned tl
 }
 
 // ---------------------------------------------------------------------------------------------
-// Backward reader over a global stream for one lane: W holds bits [wlo, wlo + 64) (wlo a multiple of
-// 32), nx the 32 bits below it, loaded one refill ahead.  Bits outside [0, 8*sl) read as zero.
+// Four bytes of a stream of sl bytes at bytePos (any alignment); bytes outside [0, sl) read as zero.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t ld_word(const uint8_t* s, int32_t sl, int32_t bytePos)
 {
@@ -119,53 +113,22 @@ __device__ __forceinline__ uint32_t ld_word(const uint8_t* s, int32_t sl, int32_
     }
     return v;
 }
-struct GBits {
-    uint64_t W;
-    int32_t wlo;
-    uint32_t nx;
-};
-__device__ __forceinline__ void gbits_init(GBits& g, const uint8_t* s, int32_t sl, int32_t q)
-{
-    g.wlo = ((q >> 5) - 1) * 32;
-    const int32_t b = g.wlo >> 3;
-    g.W = (uint64_t)ld_word(s, sl, b) | ((uint64_t)ld_word(s, sl, b + 4) << 32);
-    g.nx = ld_word(s, sl, b - 4);
-}
-// the tl bits just below q (q decreases by at most tl between calls)
-__device__ __forceinline__ uint32_t gbits_peek(GBits& g, const uint8_t* s, int32_t sl, int32_t q, unsigned tl)
-{
-    if (q - (int32_t)tl < g.wlo) {
-        g.W = (g.W << 32) | g.nx;
-        g.wlo -= 32;
-        g.nx = ld_word(s, sl, (g.wlo >> 3) - 4);
-    }
-    return (uint32_t)(g.W >> (q - (int32_t)tl - g.wlo)) & ((1u << tl) - 1u);
-}
-
-// Round staging: round r of a lane covers q in (hi - 512, hi] and stages bytes [base, base + 80)
-// with base = 4 * floor((hi - 528) / 32), so bits [q - tl, q) are always inside.
-__device__ __forceinline__ int32_t round_base(int32_t hi) { return ((hi - kRoundBits - 16) >> 5) * 4; }
-__device__ __forceinline__ void round_load(uint4 v[5], const uint8_t* s, int32_t sl, int32_t base)
+// Round staging: a lane's window of a round is (hi - W, hi] for an hi up to 11 bits below the
+// estimate it was staged for; it stages bytes [base, base + 48) with base = 4 * floor((est - W -
+// 32) / 32), so bits [q - tl, q) of every q in the window and the 64-bit reads above them are inside.
+__device__ __forceinline__ int32_t round_base(int32_t hi) { return ((hi - kWinBits - 32) >> 5) * 4; }
+__device__ __forceinline__ void round_load(uint4 v[3], const uint8_t* s, int32_t sl, int32_t base)
 {
     if (base >= 0 && base + 4 * kStgWords <= sl) {
 #pragma unroll
-        for (int i = 0; i < 5; i++) v[i] = gld<uint4>(s + base + 16 * i);
+        for (int i = 0; i < 3; i++) v[i] = gld<uint4>(s + base + 16 * i);
     } else {
 #pragma unroll
-        for (int i = 0; i < 5; i++)
+        for (int i = 0; i < 3; i++)
             v[i] = make_uint4(ld_word(s, sl, base + 16 * i), ld_word(s, sl, base + 16 * i + 4),
                               ld_word(s, sl, base + 16 * i + 8), ld_word(s, sl, base + 16 * i + 12));
     }
 }
-// the tl bits below local bit position x (x - tl >= 0) of the lane's staged bytes
-__device__ __forceinline__ uint32_t stg_peek(int lane, int32_t x, unsigned tl)
-{
-    const int32_t lo = x - (int32_t)tl;
-    const int32_t w = lo >> 5;
-    const uint64_t v = (uint64_t)sDec.stg[w][lane] | ((uint64_t)sDec.stg[w + 1][lane] << 32);
-    return (uint32_t)(v >> (lo & 31)) & ((1u << tl) - 1u);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Huffman table description (HUF_readStats + HUF_readDTableX1), wave-uniform over an LDS copy.
 // ---------------------------------------------------------------------------------------------
@@ -471,348 +434,11 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
     return used;
 }
 
-// ---------------------------------------------------------------------------------------------
-// Four Huffman streams decoded by the whole wave: 16 lanes per stream.  Each lane decodes a bit
-// range of its stream from an assumed codeword boundary (phase 1), keeping the symbols in its
-// scratch slice and its first boundaries in LDS.  One lane per stream then walks the true path
-// across the 15 lane borders (phase 2): where it meets a boundary the neighbour recorded, the
-// neighbour's speculative symbols from there on are the true ones; the few symbols before that
-// point are written by the walker.  Finally every lane copies its synchronised symbols into place
-// (phase 3).  Returns false on a malformed stream.
-// ---------------------------------------------------------------------------------------------
-// the walker's bit peek over HBM: the tl bits below q (bits below the stream start read as zero)
-__device__ __forceinline__ uint32_t walk_peek_g(const uint8_t* s, int32_t sl, int32_t q, unsigned tl)
-{
-    const int32_t lo = q - (int32_t)tl;
-    const uint32_t mask = (1u << tl) - 1u;
-    if (lo < 0) {
-        uint32_t v = 0;
-        for (int k = 0; k < 2; k++)
-            if (k < sl) v |= (uint32_t)gb(s + k) << (8 * k);
-        v &= (1u << q) - 1u;
-        return (v << (-lo)) & mask;
-    }
-    const int32_t b = lo >> 3;
-    uint32_t v = 0;
-    for (int k = 0; k < 3; k++)
-        if (b + k < sl) v |= (uint32_t)gb(s + b + k) << (8 * k);
-    return (v >> (lo & 7)) & mask;
-}
+}  // namespace pgn
 
-// the same from the lane's own border bytes [Sl/8 - kBndBelow, Sl/8 - kBndBelow + kBnd), kept in
-// registers, when they cover [q - tl, q)
-__device__ __forceinline__ uint32_t bw_word(const uint32_t (&bw)[kBnd / 4], int32_t w)
-{
-    uint32_t v = 0;
-#pragma unroll
-    for (int i = 0; i < kBnd / 4; i++) v = (w == i) ? bw[i] : v;
-    return v;
-}
-__device__ __forceinline__ uint32_t walk_peek_own(const uint32_t (&bw)[kBnd / 4], int32_t Sl, const uint8_t* s, int32_t sl,
-                                                  int32_t q, unsigned tl)
-{
-    const int32_t lo = q - (int32_t)tl;
-    const int32_t i0 = (lo >> 3) - ((Sl >> 3) - kBndBelow);
-    if (lo < 0 || i0 < 0 || i0 + 2 >= kBnd) return walk_peek_g(s, sl, q, tl);
-    const int32_t w = i0 >> 2;
-    const uint64_t v = (uint64_t)bw_word(bw, w) | ((uint64_t)bw_word(bw, w + 1) << 32);
-    return (uint32_t)(v >> (8 * (i0 & 3) + (lo & 7))) & ((1u << tl) - 1u);
-}
+#include "pgn_huf4.h"
 
-__device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                              uint8_t* htmp, uint32_t* xch, PhaseProf& P)
-{
-    const int lane = lane_id();
-    tl = uni(tl);
-    hp = uni(hp);
-    remain = uni((uint64_t)remain);
-    dst = uni(dst);
-    rs = uni(rs);
-    htmp = uni(htmp);
-    xch = uni(xch);
-    const int k = lane >> 4, j = lane & 15;
-    if (remain < 6) return false;
-    const size_t l1 = gld<uint16_t>(hp), l2 = gld<uint16_t>(hp + 2), l3 = gld<uint16_t>(hp + 4);
-    if (l1 + l2 + l3 + 6 > remain) return false;
-    const size_t l4 = remain - 6 - l1 - l2 - l3;
-    const uint32_t seg = (rs + 3) / 4;
-    if (seg * 3 > rs) return false;
-    const size_t so = (k == 0) ? 0 : (k == 1 ? l1 : (k == 2 ? l1 + l2 : l1 + l2 + l3));
-    const int32_t sl = (int32_t)((k == 0) ? l1 : (k == 1 ? l2 : (k == 2 ? l3 : l4)));
-    const uint32_t nsym = (k == 3) ? rs - 3 * seg : seg;
-    const uint8_t* src = hp + 6 + so;
-    const uint8_t lastB = sl > 0 ? gb(src + sl - 1) : 0;
-    if (ballot(lastB == 0)) return false;
-    const int32_t B = (sl - 1) * 8 + (int32_t)z1::highbit32(lastB);
-    const int32_t Lr = (B + 15) >> 4;
-    const int32_t S = (B > j * Lr) ? B - j * Lr : 0;
-    const int32_t E = (B > (j + 1) * Lr) ? B - (j + 1) * Lr : 0;
-    // border bytes for the walk
-    uint32_t bw[kBnd / 4];
-    {
-        const int32_t b0 = (S >> 3) - kBndBelow;
-#pragma unroll
-        for (int w = 0; w < kBnd / 4; w++) bw[w] = ld_word(src, sl, b0 + 4 * w);
-    }
-    // ---- phase 1: speculative decode of (E, S] into the lane's slice
-#pragma unroll
-    for (int w = 0; w < kBmpBits / 32; w++) sDec.bmp[w][lane] = 0;
-    uint8_t* slice = htmp + (size_t)lane * kSliceCap;
-    const uint32_t tmask = (1u << tl) - 1u;
-    int32_t q = S;
-    uint32_t stored = 0, npend = 0;  // symbols stored to the slice / held in pend
-    uint64_t pend = 0;
-    // full dwords wait in a 16-byte accumulator and leave as one aligned 16-byte store: a lane's
-    // slice line is then written in 8 whole pieces instead of 32 (fewer partially dirty L2 lines)
-    uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, na = 0;
-    auto push = [&](uint32_t w) {
-        a0 = na == 0 ? w : a0;
-        a1 = na == 1 ? w : a1;
-        a2 = na == 2 ? w : a2;
-        a3 = na == 3 ? w : a3;
-        if (++na == 4) {
-            if (stored + 16 <= kSliceCap) gst<uint4>(slice + stored, make_uint4(a0, a1, a2, a3));
-            stored += 16;
-            na = 0;
-        }
-    };
-    {
-        const int32_t rounds = (int32_t)wave_max((uint32_t)((S - E + kRoundBits - 1) / kRoundBits));
-        uint4 nx[5];
-        round_load(nx, src, sl, round_base(S));
-        for (int32_t r = 0; r < rounds; r++) {
-            const int32_t hi = S - r * kRoundBits;
-            const int32_t base = round_base(hi);
-#pragma unroll
-            for (int i = 0; i < 5; i++) {
-                sDec.stg[4 * i][lane] = nx[i].x;
-                sDec.stg[4 * i + 1][lane] = nx[i].y;
-                sDec.stg[4 * i + 2][lane] = nx[i].z;
-                sDec.stg[4 * i + 3][lane] = nx[i].w;
-            }
-            if (r + 1 < rounds) round_load(nx, src, sl, round_base(hi - kRoundBits));  // next round, in flight
-            lds_sync();
-            const int32_t lo = (hi - kRoundBits > E) ? hi - kRoundBits : E;
-            const int32_t b8 = 8 * base;
-            // register window: W = staged bits [wlo, wlo + 64), nxw = the word below it
-            int32_t wi = (q - b8 - (int32_t)tl) >> 5;
-            wi = wi < 0 ? 0 : (wi > kStgWords - 2 ? kStgWords - 2 : wi);
-            int32_t wlo = 32 * wi;
-            uint64_t W = (uint64_t)sDec.stg[wi][lane] | ((uint64_t)sDec.stg[wi + 1][lane] << 32);
-            uint32_t nxw = sDec.stg[wi > 0 ? wi - 1 : 0][lane];
-            auto step = [&](bool act) {
-                const int32_t x = q - b8 - (int32_t)tl;
-                const bool rf = x < wlo;
-                W = rf ? ((W << 32) | nxw) : W;
-                wlo = rf ? wlo - 32 : wlo;
-                nxw = sDec.stg[wlo >= 64 ? (wlo >> 5) - 1 : 0][lane];
-                const uint32_t e = sDec.tab[(uint32_t)(W >> ((x - wlo) & 63)) & tmask];
-                q = act ? q - (int32_t)(e >> 8) : q;
-                pend |= act ? ((uint64_t)(e & 0xFFu) << (8 * npend)) : 0ull;
-                npend += act ? 1u : 0u;
-            };
-            auto flush4 = [&]() {
-                if (npend >= 4) {
-                    push((uint32_t)pend);
-                    pend >>= 32;
-                    npend -= 4;
-                }
-            };
-            // the first kBmpBits bits below S: record every codeword boundary for the walk
-            while (q > lo && S - q < kBmpBits) {
-                const int32_t d = S - q;
-                atomicOr(&sDec.bmp[d >> 5][lane], 1u << (d & 31));
-                step(true);
-                flush4();
-            }
-            // fast path: every lane still has >= 4 * tl bits in this round, so four symbols decode
-            // unpredicated, with one refill check per pair (2 * tl <= 32 - tl for tl <= 12)
-            const int32_t xb = b8 + (int32_t)tl, tli = (int32_t)tl;
-            while (!ballot(q - lo < 4 * tli)) {
-                uint32_t word = 0;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const bool rf = (q - xb) - wlo < tli;
-                    W = rf ? ((W << 32) | nxw) : W;
-                    wlo = rf ? wlo - 32 : wlo;
-                    nxw = sDec.stg[wlo >= 64 ? (wlo >> 5) - 1 : 0][lane];
-#pragma unroll
-                    for (int u = 0; u < 2; u++) {
-                        const uint32_t e = sDec.tab[(uint32_t)(W >> ((q - xb) - wlo)) & tmask];
-                        q -= (int32_t)(e >> 8);
-                        word |= (e & 0xFFu) << (8 * (2 * h + u));
-                    }
-                }
-                pend |= (uint64_t)word << (8 * npend);
-                push((uint32_t)pend);
-                pend >>= 32;
-            }
-            while (ballot(q > lo)) {
-#pragma unroll
-                for (int u = 0; u < 4; u++) step(q > lo);
-                flush4();
-            }
-            lds_sync();
-        }
-        // the accumulator's dwords, then the pending bytes
-        for (uint32_t t = 0; t < na; t++) {
-            const uint32_t w = t == 0 ? a0 : (t == 1 ? a1 : a2);
-            if (stored + 4 <= kSliceCap) gst<uint32_t>(slice + stored, w);
-            stored += 4;
-        }
-        for (uint32_t t = 0; t < npend; t++)
-            if (stored + t < kSliceCap) gst<uint8_t>(slice + stored + t, (uint8_t)(pend >> (8 * t)));
-    }
-    const uint32_t c = stored + npend;
-    P.mark(11);
-    // ---- phase 2: the border walks.  If lane l-1 synchronised, the true path enters lane l's range
-    // at l-1's speculative exit, so all 15 walks of a stream run at once; the walk symbols wait in
-    // the (now free) staging row.  A stream with a lane that does not meet its boundaries within
-    // kBmpBits bits falls back to the serial walker.
-    // walk symbols: byte t of the lane at word t / 4 of its (now free) staging column
-    auto wsym_at = [&](uint32_t t) -> uint8_t& { return ((uint8_t*)&sDec.stg[t >> 2][lane])[t & 3]; };
-    constexpr uint32_t kWalkMax = 4 * kStgWords;
-    uint32_t ex = 0;
-    const int32_t prevExit = (int32_t)dpp<kDppRowShr1>((uint32_t)q);  // lane l-1's exit (rows = streams)
-    int32_t p = (j == 0) ? S : prevExit;
-    bool synced = (j == 0);
-    if (j > 0) {
-        while (p > E && ex < kWalkMax) {
-            const int32_t d = S - p;
-            if (d >= kBmpBits) break;
-            if ((sDec.bmp[d >> 5][lane] >> (d & 31)) & 1u) { synced = true; break; }
-            const uint32_t e = sDec.tab[walk_peek_own(bw, S, src, sl, p, tl)];
-            p -= (int32_t)(e >> 8);
-            wsym_at(ex++) = (uint8_t)e;
-        }
-    }
-    const int32_t dsync = S - p;
-    uint32_t idx = 0;
-    if (synced && j > 0) {
-        for (int w = 0; w < (dsync >> 5); w++) idx += (uint32_t)__builtin_popcount(sDec.bmp[w][lane]);
-        if (dsync & 31) idx += (uint32_t)__builtin_popcount(sDec.bmp[dsync >> 5][lane] & ((1u << (dsync & 31)) - 1u));
-    }
-    const uint64_t unsynced = ballot(!synced);
-    const bool fast = ((unsynced >> (16 * k)) & 0xFFFFull) == 0;
-    uint8_t* sdst = dst + (size_t)seg * (size_t)k;
-    // this lane's placement: skip its first sk speculative symbols, write exl walk symbols at ob
-    uint32_t sk = idx, syncd = (uint32_t)dsync, exl = ex, ob = 0;
-    {
-        const uint32_t tc = ex + (c - idx);
-        uint32_t incl = tc;  // inclusive sum over the stream's 16 lanes (one DPP row)
-        incl += dpp<kDppRowShr1>(incl);
-        incl += dpp<kDppRowShr2>(incl);
-        incl += dpp<kDppRowShr4>(incl);
-        incl += dpp<kDppRowShr8>(incl);
-        ob = incl - tc;
-        if (fast && j == 15) {
-            sDec.u[8 + k] = incl;
-            sDec.u[12 + k] = (uint32_t)q;  // true end of the stream (must be 0)
-        }
-    }
-    if (unsynced) {
-        // serial fallback: one lane per such stream walks the 15 borders in order, over the lanes'
-        // values exchanged through HBM (a wave's vector-memory accesses are performed in order)
-        uint32_t* X = xch;
-        X[lane] = c;
-        X[64 + lane] = (uint32_t)S;
-        X[128 + lane] = (uint32_t)E;
-        X[192 + lane] = (uint32_t)q;
-        wave_sync();
-        if (!fast && j == 0) {
-            X[256 + lane] = 0;  // obase, skip, syncd, extra of the stream's first lane
-            X[320 + lane] = 0;
-            X[384 + lane] = 0;
-            X[448 + lane] = 0;
-            uint32_t out = c;  // symbols placed so far in this stream
-            int32_t T = q;
-            for (int jj = 1; jj < 16; jj++) {
-                const int l = lane + jj;
-                const uint32_t cl = X[l];
-                const int32_t Sl = (int32_t)X[64 + l], El = (int32_t)X[128 + l];
-                X[256 + l] = out;
-                int32_t pp = T;
-                uint32_t exx = 0;
-                bool sy = false;
-                while (pp > El) {
-                    const int32_t d = Sl - pp;
-                    if (d >= kBmpBits) break;  // past the recorded boundaries: finish serially below
-                    if ((sDec.bmp[d >> 5][l] >> (d & 31)) & 1u) { sy = true; break; }
-                    const uint32_t e = sDec.tab[walk_peek_g(src, sl, pp, tl)];
-                    pp -= (int32_t)(e >> 8);
-                    if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
-                    exx++;
-                }
-                if (sy) {
-                    const int32_t d = Sl - pp;
-                    uint32_t ix = 0;
-                    for (int w = 0; w < (d >> 5); w++) ix += (uint32_t)__builtin_popcount(sDec.bmp[w][l]);
-                    if (d & 31) ix += (uint32_t)__builtin_popcount(sDec.bmp[d >> 5][l] & ((1u << (d & 31)) - 1u));
-                    X[320 + l] = ix;
-                    X[384 + l] = (uint32_t)d;
-                    T = (int32_t)X[192 + l];
-                    out += exx + (cl - ix);
-                } else {  // no common boundary: the walker decodes the rest of the range itself
-                    while (pp > El) {
-                        const uint32_t e = sDec.tab[walk_peek_g(src, sl, pp, tl)];
-                        pp -= (int32_t)(e >> 8);
-                        if (out + exx < nsym) gst<uint8_t>(sdst + out + exx, (uint8_t)e);
-                        exx++;
-                    }
-                    X[320 + l] = cl;
-                    X[384 + l] = 0;
-                    T = pp;
-                    out += exx;
-                }
-                X[448 + l] = exx;
-            }
-            sDec.u[12 + k] = (uint32_t)T;
-            sDec.u[8 + k] = out;
-        }
-        wave_sync();
-        if (!fast) {
-            ob = X[256 + lane];
-            sk = X[320 + lane];
-            syncd = X[384 + lane];
-            exl = X[448 + lane];
-        }
-    }
-    lds_sync();
-    P.mark(12);
-    const bool good = (sDec.u[8 + k] == nsym) && ((int32_t)sDec.u[12 + k] == 0);
-    if (ballot(!good)) return false;
-    // ---- phase 3: walk symbols and the synchronised speculative symbols into place
-    if (fast)
-        for (uint32_t t = 0; t < exl; t++) gst<uint8_t>(sdst + ob + t, wsym_at(t));
-    const uint32_t o = ob + exl;
-    if (c > sk) {
-        const uint32_t len = c - sk;
-        if (c <= kSliceCap) {
-            const uint8_t* from = slice + sk;
-            uint8_t* to = sdst + o;
-            uint32_t t = 0;
-            for (; t + 64 <= len; t += 64) {
-                uint4 v[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) v[u] = gld<uint4>(from + t + 16 * u);
-#pragma unroll
-                for (int u = 0; u < 4; u++) gst<uint4>(to + t + 16 * u, v[u]);
-            }
-            for (; t + 4 <= len; t += 4) gst<uint32_t>(to + t, gld<uint32_t>(from + t));
-            for (; t < len; t++) gst<uint8_t>(to + t, gb(from + t));
-        } else {  // slice overflow: decode again from the synchronisation point
-            int32_t pp = S - (int32_t)syncd;
-            GBits g;
-            gbits_init(g, src, sl, pp);
-            for (uint32_t t = 0; t < len; t++) {
-                const uint32_t e = sDec.tab[gbits_peek(g, src, sl, pp, tl)];
-                pp -= (int32_t)(e >> 8);
-                gst<uint8_t>(sdst + o + t, (uint8_t)e);
-            }
-        }
-    }
-    return true;
-}
+namespace pgn {
 
 // Four streams with a 12-bit table (HBM): one lane per stream decodes serially.  zstd's own
 // encoders never write such tables; this path exists for completeness of the format.
@@ -1171,12 +797,10 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     dst = uni(dst);
     dstCap = uni((uint64_t)dstCap);
     S.lit = uni(S.lit);
-    S.htmp = uni(S.htmp);
     S.seqs = uni(S.seqs);
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
     S.htab = uni(S.htab);
-    S.xch = uni(S.xch);
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
     while (ip < srcSize) {
@@ -1309,7 +933,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     } else if (gt) {
                         ok = huf_decode4_serial(hufTl, hp, remain, litOut, (uint32_t)rs, gt);
                     } else {
-                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, S.htmp, S.xch, P);
+                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, P);
                     }
                     if (ballot(!ok)) return z1::kDecErrHufStream;
                     P.mark(2);

@@ -13,7 +13,7 @@ from rawnanoporesignalcompression_amd import PGNanoCodec
 ENC = ["split", "search", "lit_gather", "hist", "sort", "hdr(writeCTable)", "huf_encode", "raw_lit", "seq",
        "frame_finish", "assemble", "tree_merge", "tree_depth", "tree_maxheight", "tree_canon"]
 DEC = ["parse/merge_wait", "huf_table", "huf_copy(ph3)", "seq_list", "seq_exec", "raw_copy", "merge",
-       "lit_hdr", "-", "-", "-", "huf_spec(ph1)", "huf_walk(ph2)"]
+       "lit_hdr", "huf_store(passB)", "-", "-", "huf_spec(passA)", "huf_sync"]
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 S = 100000
 c = PGNanoCodec(0)
