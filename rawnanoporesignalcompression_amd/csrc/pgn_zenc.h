@@ -379,13 +379,17 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
     lds_sync();
     uint32_t winLo = 0;   // bit offset of win[0] (multiple of 32)
     uint32_t bitBase = 0; // bits emitted before this step
+    // the next step's 16-byte block is loaded one step ahead
+    uint4 nv = make_uint4(0, 0, 0, 0);
+    if ((int32_t)len - 16 - (int32_t)(16 * lane) >= 0) nv = gld<uint4>(src + (len - 16 - 16 * lane));
     for (uint32_t r0 = 0; r0 < len; r0 += 1024) {
         // my 16 emissions r0 + 16*lane + j are bytes len-1-r of src: one 16-byte block, reversed
         const int32_t a = (int32_t)len - 16 - (int32_t)(r0 + 16 * lane);
         uint32_t wv[4];
         if (a >= 0) {
-            const uint4 v = gld<uint4>(src + a);
+            const uint4 v = nv;
             wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
+            if (a - 1024 >= 0) nv = gld<uint4>(src + (a - 1024));
         } else {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -1163,22 +1167,33 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     const int nseg = single ? 1 : 4;
     for (int i = lane; i < 2 * 256; i += 64) (&L.hist2[0][0])[i] = 0;
     wave_sync();
-    // per-segment histograms
-    for (uint32_t i = (uint32_t)lane * 16; i < n; i += 1024) {
-        uint8_t b[16];
-        if (i + 16 <= n) {
-            const uint4 v = gld<uint4>(lit + i);
-            __builtin_memcpy(b, &v, 16);
-        } else {
-            for (int k = 0; k < 16; k++) b[k] = (i + k < n) ? gb(lit + i + k) : 0;
-        }
-        uint32_t sa = i / segSize;
-        uint32_t boundary = (sa + 1) * segSize;
+    // per-segment histograms; the 16-byte loads of four 1024-byte steps are issued together
+    for (uint32_t i0 = (uint32_t)lane * 16; i0 < n; i0 += 4096) {
+        uint4 v[4];
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            if (i + k < n) {
-                uint32_t sg = (i + k < boundary) ? sa : sa + 1;
-                atomicAdd(&L.hist2[sg >> 1][b[k]], 1u << (16 * (sg & 1)));
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 1024u * (uint32_t)u;
+            if (i + 16 <= n) {
+                v[u] = gld<uint4>(lit + i);
+            } else {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (uint32_t k = 0; k < 16; k++)
+                    if (i + k < n) w[k >> 2] |= (uint32_t)gb(lit + i + k) << (8 * (k & 3));
+                v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 1024u * (uint32_t)u;
+            const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            const uint32_t sa = i / segSize;
+            const uint32_t boundary = (sa + 1) * segSize;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if (i + k < n) {
+                    const uint32_t sg = (i + k < boundary) ? sa : sa + 1;
+                    atomicAdd(&L.hist2[sg >> 1][(wd[k >> 2] >> (8 * (k & 3))) & 0xFFu], 1u << (16 * (sg & 1)));
+                }
             }
         }
     }
