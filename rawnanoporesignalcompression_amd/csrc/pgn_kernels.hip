@@ -586,12 +586,12 @@ struct pgn_ctx {
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
     uint32_t* epochs = nullptr;
-    uint8_t* encChunks = nullptr;  // G * (kChunkStreamBytes + kChunkFrameBytes) + sizes + fsizes
-    size_t encG = 0;
+    uint8_t* encChunks = nullptr;  // per buffer: G * (kChunkStreamBytes + kChunkFrameBytes) + sizes + fsizes
+    size_t encG = 0;               // chunk capacity of all buffers together
     // decode
     uint8_t* decScratch = nullptr;
     size_t decSlots = 0;
-    uint8_t* decChunks = nullptr;  // G * kChunkInterBytes + units
+    uint8_t* decChunks = nullptr;  // per buffer: G * kChunkInterBytes + units
     size_t decG = 0;
     DecUnit* lastUnits = nullptr;  // decode records of the last pass (diagnostics)
     uint32_t* queues = nullptr;    // one work counter per sub-batch pass
@@ -600,6 +600,11 @@ struct pgn_ctx {
     uint8_t* stage = nullptr;
     size_t stageBytes = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // two-stream pipeline over sub-batches (launch_encode / launch_decode): the side stream runs the
+    // split (encode) or the merge (decode) of one sub-batch while the caller's stream runs the zstd
+    // kernel of the neighbouring one; two per-chunk buffers alternate between sub-batches
+    hipStream_t side = nullptr;
+    hipEvent_t evFork = nullptr, evJoin = nullptr, evStage[2] = {nullptr, nullptr}, evFree[2] = {nullptr, nullptr};
     uint64_t* prof = nullptr;  // [2][kPhases] phase cycles (encode, decode) when PGN_PHASE_PROFILE=1
     bool encTimed = false, decTimed = false;
     std::mutex mu;
@@ -663,6 +668,10 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&decPerCU, dec_zstd_kernel, 64, 0));
     if (encPerCU < 1) encPerCU = 1;
     if (decPerCU < 1) decPerCU = 1;
+    // resident zstd workgroups per CU (tuning knobs PGN_ENC_WG_PER_CU / PGN_DEC_WG_PER_CU: fewer
+    // leave room for the side stream's split / merge kernels)
+    if (const char* v = getenv("PGN_ENC_WG_PER_CU")) { const int x = atoi(v); if (x > 0 && x < encPerCU) encPerCU = x; }
+    if (const char* v = getenv("PGN_DEC_WG_PER_CU")) { const int x = atoi(v); if (x > 0 && x < decPerCU) decPerCU = x; }
     c->encSlotsMax = (size_t)c->numCUs * (size_t)(encPerCU > 32 ? 32 : encPerCU);
     c->decSlotsMax = (size_t)c->numCUs * (size_t)(decPerCU > 32 ? 32 : decPerCU);
     if (const char* sb = getenv("PGN_SUBBATCH")) {
@@ -677,6 +686,13 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         HIPCHK(hipDeviceSynchronize());
     }
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming));
+    for (int i = 0; i < 2; i++) {
+        HIPCHK(hipEventCreateWithFlags(&c->evStage[i], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->evFree[i], hipEventDisableTiming));
+    }
     // the predefined sequence FSE tables of the decoder (one wave, once per context)
     hipLaunchKernelGGL(seq_default_tables_kernel, dim3(1), dim3(64), 0, c->stream);
     HIPCHK(hipGetLastError());
@@ -699,6 +715,10 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->stage);
     (void)hipFree(c->prof);
     for (int i = 0; i < 4; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    for (hipEvent_t e : {c->evFork, c->evJoin, c->evStage[0], c->evStage[1], c->evFree[0], c->evFree[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (c->side) (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return PGN_OK;
@@ -724,8 +744,8 @@ static int ensure_enc(pgn_ctx* c, size_t slots, size_t G)
         HIPCHK(hipStreamSynchronize(c->stream));
         c->encSlots = slots;
     }
-    if (G > c->encG) {
-        (void)hipStreamSynchronize(c->stream);
+    if (G > c->encG) {  // G = chunk capacity over all buffers
+        (void)hipDeviceSynchronize();
         (void)hipFree(c->encChunks);
         c->encChunks = nullptr;
         HIPCHK(hipMalloc(&c->encChunks, G * (kChunkStreamBytes + kChunkFrameBytes + 2 * 4 * kStreams)));
@@ -743,8 +763,8 @@ static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
         HIPCHK(hipMalloc(&c->decScratch, dec_layout().bytes * slots));
         c->decSlots = slots;
     }
-    if (G > c->decG) {
-        (void)hipStreamSynchronize(c->stream);
+    if (G > c->decG) {  // G = chunk capacity over all buffers
+        (void)hipDeviceSynchronize();
         (void)hipFree(c->decChunks);
         c->decChunks = nullptr;
         HIPCHK(hipMalloc(&c->decChunks, G * (kChunkInterBytes + kStreams * sizeof(DecUnit))));
@@ -779,11 +799,15 @@ static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d
     const size_t passes = (nchunks + G - 1) / G;
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
     const size_t slots = nu * G < c->encSlotsMax ? nu * G : c->encSlotsMax;
-    int rc = ensure_enc(c, slots, G);
+    const size_t nbuf = passes > 1 ? 2 : 1;
+    int rc = ensure_enc(c, slots, nbuf * G);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[0], s));
     rc = ensure_queues(c, passes, s);
     if (rc) return rc;
+    HIPCHK(hipEventRecord(c->evFork, s));
+    HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
+    const size_t bufBytes = G * (kChunkStreamBytes + kChunkFrameBytes + 2 * 4 * kStreams);
     EncArgs a;
     a.nchunks = nchunks;
     a.samples = d_samples;
@@ -795,28 +819,33 @@ static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d
     a.outSizes = d_out_sizes;
     a.status = d_status;
     a.stats = d_stats;
-    a.streams = c->encChunks;
-    a.frames = c->encChunks + G * kChunkStreamBytes;
-    a.sizes = (uint32_t*)(a.frames + G * kChunkFrameBytes);
-    a.fsizes = a.sizes + G * kStreams;
     a.slotScratch = c->encScratch;
     a.slotBytes = enc_layout().bytes;
     a.epochs = c->epochs;
     a.prof = c->prof;
     a.G = G;
     a.nu = nu;
+    // pass p: split on the side stream into buffer p % 2; zstd + assemble on the caller's stream.
+    // The split of pass p+1 overlaps the zstd kernel of pass p; a buffer is split into again only
+    // after the assemble kernel of the pass before last has read it.
     for (size_t p = 0; p < passes; p++) {
+        const int b = (int)(p & 1);
+        uint8_t* buf = c->encChunks + (size_t)b * bufBytes;
+        a.streams = buf;
+        a.frames = buf + G * kChunkStreamBytes;
+        a.sizes = (uint32_t*)(a.frames + G * kChunkFrameBytes);
+        a.fsizes = a.sizes + G * kStreams;
         a.base = p * G;
         a.queue = c->queues + p;
-        if (codec == kCodecVbz) {
-            hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(vbz_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-        } else {
-            hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-        }
+        if (p >= 2) HIPCHK(hipStreamWaitEvent(c->side, c->evFree[b], 0));
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
+        else hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
+        HIPCHK(hipEventRecord(c->evStage[b], c->side));
+        HIPCHK(hipStreamWaitEvent(s, c->evStage[b], 0));
+        hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        HIPCHK(hipEventRecord(c->evFree[b], s));
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
@@ -834,11 +863,15 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     const size_t passes = (nchunks + G - 1) / G;
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
     const size_t slots = nu * G < c->decSlotsMax ? nu * G : c->decSlotsMax;
-    int rc = ensure_dec(c, slots, G);
+    const size_t nbuf = passes > 1 ? 2 : 1;
+    int rc = ensure_dec(c, slots, nbuf * G);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[2], s));
     rc = ensure_queues(c, passes, s);
     if (rc) return rc;
+    HIPCHK(hipEventRecord(c->evFork, s));
+    HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
+    const size_t bufBytes = G * (kChunkInterBytes + kStreams * sizeof(DecUnit));
     DecArgs a;
     a.nchunks = nchunks;
     a.in = d_in;
@@ -848,28 +881,35 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     a.sampleOffsets = d_sample_offsets;
     a.sampleCounts = d_sample_counts;
     a.status = d_status;
-    a.inter = c->decChunks;
-    a.units = (DecUnit*)(c->decChunks + G * kChunkInterBytes);
-    c->lastUnits = a.units;
     a.slotScratch = c->decScratch;
     a.slotBytes = dec_layout().bytes;
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.G = G;
     a.nu = nu;
+    // pass p: parse + zstd on the caller's stream into buffer p % 2, merge on the side stream.  The
+    // merge of pass p overlaps the zstd kernel of pass p+1; a buffer is parsed into again only after
+    // the merge of the pass before last has read it.
     for (size_t p = 0; p < passes; p++) {
+        const int b = (int)(p & 1);
+        uint8_t* buf = c->decChunks + (size_t)b * bufBytes;
+        a.inter = buf;
+        a.units = (DecUnit*)(buf + G * kChunkInterBytes);
+        c->lastUnits = a.units;
         a.base = p * G;
         a.queue = c->queues + p;
-        if (codec == kCodecVbz) {
-            hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-        } else {
-            hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-            hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-        }
+        if (p >= 2) HIPCHK(hipStreamWaitEvent(s, c->evFree[b], 0));
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+        HIPCHK(hipEventRecord(c->evStage[b], s));
+        HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
+        else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
+        HIPCHK(hipEventRecord(c->evFree[b], c->side));
     }
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->evJoin, c->side));
+    HIPCHK(hipStreamWaitEvent(s, c->evJoin, 0));
     HIPCHK(hipEventRecord(c->ev[3], s));
     c->decTimed = true;
     return PGN_OK;
