@@ -210,8 +210,7 @@ def main():
         # the hot path is a three-kernel pipeline per direction; the roofline is taken over the dominant
         # direction's launch sequence (HIP events on the codec stream around all its kernels)
         dominant = "c5_decode" if d_ms >= e_ms else "c5_encode"
-        kernels = {"c5_encode": "enc_split_kernel + enc_zstd_kernel + enc_assemble_kernel",
-                   "c5_decode": "dec_parse_kernel + dec_zstd_kernel + dec_merge_kernel"}[dominant]
+        kernels = codec.kernels(1 if dominant == "c5_decode" else 0)
         k_ms = max(e_ms, d_ms)
         algo_bytes = (2.0 + comp_bytes / (R * S)) * R * S  # per launch on this GPU
         achieved = algo_bytes / (k_ms * 1e-3) / 1e9

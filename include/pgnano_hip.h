@@ -133,6 +133,10 @@ int pgn_debug_phase_cycles(pgn_ctx *ctx, uint64_t *out, int n);
  * u32 intermediate offset, i32 decoded bytes or a negative error). */
 int pgn_debug_decode_units(pgn_ctx *ctx, void *out, size_t nchunks);
 
+/* Kernels of the C5 batch path on ctx, direction 0 = encode, 1 = decode: the fused per-chunk kernel
+ * or the staged three-kernel pipeline (PGN_ENC_PIPELINE / PGN_DEC_PIPELINE = fused | staged). */
+const char *pgn_ctx_kernels(pgn_ctx *ctx, int direction);
+
 /* Kernel time (ms, HIP events on the launch stream) of the last batch encode / decode call on ctx. */
 float pgn_ctx_last_encode_ms(pgn_ctx *ctx);
 float pgn_ctx_last_decode_ms(pgn_ctx *ctx);

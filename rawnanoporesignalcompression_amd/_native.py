@@ -55,6 +55,7 @@ SIGNATURES = [
       _VP]),
     ("pgn_debug_phase_cycles", C.c_int, [_VP, _VP, C.c_int]),
     ("pgn_debug_decode_units", C.c_int, [_VP, _VP, C.c_size_t]),
+    ("pgn_ctx_kernels", C.c_char_p, [_VP, C.c_int]),
     ("pgn_ctx_last_encode_ms", C.c_float, [_VP]),
     ("pgn_ctx_last_decode_ms", C.c_float, [_VP]),
 ]

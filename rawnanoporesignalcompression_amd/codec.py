@@ -213,6 +213,10 @@ class PGNanoCodec:
                                                 _ptr(counts), p_switch_q16, level_mean, level_sd, noise_sd, 0))
         return out, offs, counts
 
+    def kernels(self, direction: int) -> str:
+        """Kernel names of the C5 batch path (0 = encode, 1 = decode)."""
+        return self._lib.pgn_ctx_kernels(self._h, int(direction)).decode()
+
     def last_encode_ms(self) -> float:
         return float(self._lib.pgn_ctx_last_encode_ms(self._h))
 

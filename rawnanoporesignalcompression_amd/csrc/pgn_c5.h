@@ -262,9 +262,9 @@ __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, bool 
 }
 
 __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
-                                             uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint64_t* consumed)
+                                             uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint64_t* consumed,
+                                             MergeLds& W)
 {
-    __shared__ MergeLds W;
     const uint32_t lane = (uint32_t)lane_id();
     const uint64_t kl = ((uint64_t)n + 3) / 4;
     const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;

@@ -358,6 +358,7 @@ __global__ __launch_bounds__(64) void dec_merge_kernel(DecArgs a)
     const size_t c = a.base + g;
     if (g >= a.G || c >= a.nchunks) return;
     if (a.status[c] != PGN_OK) return;
+    static __shared__ MergeLds W;
     PhaseProf P;
     P.init(a.prof);
     const DecUnit* d = a.units + g * kStreams;
@@ -370,7 +371,7 @@ __global__ __launch_bounds__(64) void dec_merge_kernel(DecArgs a)
     if (st == PGN_OK) {
         uint64_t consumed = 0;
         const int bad = c5_merge_wave(a.inter + g * kChunkInterBytes, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres,
-                                      (uint64_t)d[3].dres, a.samples + a.sampleOffsets[c], a.sampleCounts[c], &consumed);
+                                      (uint64_t)d[3].dres, a.samples + a.sampleOffsets[c], a.sampleCounts[c], &consumed, W);
         if (bad) st = PGN_ERR_CORRUPT;
         else if (consumed != total) st = PGN_ERR_REMAINING;
     }
@@ -472,6 +473,7 @@ __global__ __launch_bounds__(64) void vbz_merge_kernel(DecArgs a)
     const size_t c = a.base + g;
     if (g >= a.G || c >= a.nchunks) return;
     if (a.status[c] != PGN_OK) return;
+    static __shared__ VbzMergeLds W;
     PhaseProf P;
     P.init(a.prof);
     const DecUnit* d = a.units + g * kStreams;
@@ -489,13 +491,263 @@ __global__ __launch_bounds__(64) void vbz_merge_kernel(DecArgs a)
             st = svb_key_length(n) <= total ? PGN_ERR_REMAINING : PGN_ERR_CORRUPT;
         } else {
             const int bad = vbz_merge_wave(a.inter + g * kChunkInterBytes, total, a.samples + a.sampleOffsets[c], n,
-                                           &consumed);
+                                           &consumed, W);
             if (bad) st = PGN_ERR_CORRUPT;
             else if (consumed != d->cs) st = PGN_ERR_REMAINING;
         }
     }
     if (lane_id() == 0) a.status[c] = st;
     P.mark(6);
+    P.flush();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused per-chunk pipeline (the default).  One persistent wave takes whole chunks from a queue:
+//   encode: split into its slot's stream area -> the five zstd frames written straight into the
+//           chunk's blob behind their length prefixes -> size, status, stats;
+//   decode: prefixes and frame headers -> the five frames decoded into its slot's intermediate ->
+//           merge into the samples, consumed-bytes check.
+// Waves in different stages share each CU (VALU-bound split/merge beside latency-bound entropy
+// coding), a chunk's streams are re-read by the wave that just wrote them, and frames are never
+// staged and copied.  The split/merge LDS overlays the zstd stage's (stages of one wave never
+// overlap in time).
+// ---------------------------------------------------------------------------------------------
+static_assert(sizeof(SplitLds) <= sizeof(EncLds) && sizeof(VbzSplitLds) <= sizeof(EncLds), "split LDS overlay");
+static_assert(sizeof(MergeLds) <= sizeof(DecLds) && sizeof(VbzMergeLds) <= sizeof(DecLds), "merge LDS overlay");
+
+// slot scratch of the fused kernels: the zstd scratch, then the chunk's streams (encode: + one
+// frame for a stream that may not fit the destination) or its intermediate (decode)
+__host__ __device__ inline size_t enc_slot_bytes() { return enc_layout().bytes + kChunkStreamBytes + frame_pad(2); }
+__host__ __device__ inline size_t dec_slot_bytes() { return dec_layout().bytes + kChunkInterBytes; }
+
+// The split and merge stages as non-inlined calls with wave-uniform arguments: each gets its own
+// register allocation instead of sharing the kernel's with the state kept across the zstd calls
+// (inlined, both spilled to scratch inside their step loops).
+struct SplitOut {
+    uint32_t s[kStreams];
+};
+__device__ __noinline__ SplitOut c5_split_chunk(const int16_t* x, uint32_t n, uint8_t* streams)
+{
+    x = uni(x);
+    n = uni(n);
+    streams = uni(streams);
+    C5Streams st{streams + stream_off(0), streams + stream_off(1), streams + stream_off(2), streams + stream_off(3),
+                 streams + stream_off(4)};
+    SplitOut o;
+    c5_split_wave(x, n, st, o.s, *reinterpret_cast<SplitLds*>(&sEnc));
+    return o;
+}
+__device__ __noinline__ uint32_t vbz_split_chunk(const int16_t* x, uint32_t n, uint8_t* out)
+{
+    return vbz_split_wave(uni(x), uni(n), uni(out), *reinterpret_cast<VbzSplitLds*>(&sEnc));
+}
+struct MergeOut {
+    int bad;
+    uint64_t consumed;
+};
+__device__ __noinline__ MergeOut c5_merge_chunk(const uint8_t* in, uint64_t total, uint64_t dS, uint64_t dM, uint64_t dLl,
+                                                int16_t* out, uint32_t n)
+{
+    MergeOut o{0, 0};
+    o.bad = c5_merge_wave(uni(in), uni(total), uni(dS), uni(dM), uni(dLl), uni(out), uni(n), &o.consumed,
+                          *reinterpret_cast<MergeLds*>(&sDec));
+    return o;
+}
+__device__ __noinline__ MergeOut vbz_merge_chunk(const uint8_t* in, uint64_t total, int16_t* out, uint32_t n)
+{
+    MergeOut o{0, 0};
+    o.bad = vbz_merge_wave(uni(in), uni(total), uni(out), uni(n), &o.consumed, *reinterpret_cast<VbzMergeLds*>(&sDec));
+    return o;
+}
+
+__device__ __forceinline__ void enc_fail_chunk(const EncArgs& a, size_t c, int st)
+{
+    if (lane_id() == 0) {
+        a.status[c] = st;
+        a.outSizes[c] = 0;
+    }
+}
+
+template <int Codec>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void enc_chunk_kernel(EncArgs a)
+{
+    const int lane = lane_id();
+    const EncLayout lay = enc_layout();
+    uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
+    EncScratch S;
+    S.ht = (uint32_t*)(sbase + lay.ht);
+    S.seqs = (z1::Seq*)(sbase + lay.seqs);
+    S.codes = sbase + lay.codes;
+    S.lit = sbase + lay.lit;
+    S.seqSection = sbase + lay.seqSection;
+    S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
+    S.maxSeq = kMaxEncSeq;
+    uint8_t* streams = sbase + lay.bytes;
+    uint8_t* fbuf = streams + kChunkStreamBytes;
+    uint32_t epoch = a.epochs[blockIdx.x];
+    PhaseProf P;
+    P.init(a.prof);
+    while (true) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(a.queue, 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= a.nchunks) break;
+        const size_t c = u;
+        const uint32_t n = a.sampleCounts[c];
+        if (n > kMaxSamples) {
+            enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
+            continue;
+        }
+        constexpr int nu = Codec == kCodecVbz ? 1 : kStreams;
+        uint32_t sz[kStreams] = {0, 0, 0, 0, 0};
+        const uint8_t* src[kStreams];
+        if (Codec == kCodecVbz) {
+            // the data part (after the ceil(n/8) key bytes) 16-byte aligned, as in vbz_split_kernel
+            const uint32_t pad = (16u - (svb_key_length(n) & 15u)) & 15u;
+            sz[0] = vbz_split_chunk(a.samples + a.sampleOffsets[c], n, streams + pad);
+            src[0] = streams + pad;
+            if (sz[0] > z1::kMaxSrc) {  // more than one zstd block: not on the GPU path
+                enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
+                continue;
+            }
+        } else {
+            const SplitOut so = c5_split_chunk(a.samples + a.sampleOffsets[c], n, streams);
+#pragma unroll
+            for (int s = 0; s < kStreams; s++) sz[s] = so.s[s];
+#pragma unroll
+            for (int s = 0; s < kStreams; s++) src[s] = streams + stream_off(s);
+        }
+#pragma unroll
+        for (int s = 0; s < kStreams; s++) sz[s] = uni(sz[s]);
+        P.mark(0);
+        wave_sync();
+        uint8_t* dst = a.out + a.outOffsets[c];
+        const uint64_t cap = a.outCaps[c];
+        uint64_t off = 0;
+        bool ok = true;
+        uint32_t fs[kStreams];
+#pragma unroll
+        for (int s = 0; s < nu; s++) {
+            if (Codec != kCodecVbz && s < 4) off += 8;  // C5.hpp:429-462 length prefixes (not before Lhigh)
+            if (++epoch >= 32768u) {  // tag space exhausted: clear the table once
+                for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
+                epoch = 1;
+                wave_sync();
+            }
+            // straight into the blob when the frame bound fits the capacity; otherwise through the
+            // slot's frame buffer (the reference compresses into its own buffers, then checks the
+            // total against the destination: C5.hpp:412-427, signal_compression.cpp:57-62)
+            const bool direct = ok && off + frame_bound(sz[s]) <= cap;
+            const size_t f = uni(zstd1_compress_wave(direct ? dst + off : fbuf, src[s], sz[s], S, epoch, P));
+            wave_sync();
+            if (!direct && ok) {
+                if (off + f <= cap) wave_copy(dst + off, fbuf, f);
+                else ok = false;
+                wave_sync();
+            }
+            if (Codec != kCodecVbz && s < 4 && ok && lane == 0) {
+                const uint64_t v = f;
+                __builtin_memcpy(dst + off - 8, &v, 8);
+            }
+            fs[s] = (uint32_t)f;
+            off += f;
+        }
+        P.mark(10);
+        if (lane == 0) {
+            if (Codec == kCodecVbz) {
+                a.status[c] = ok ? PGN_OK : PGN_ERR_ZSTD_COMPRESS;
+                a.outSizes[c] = ok ? off : 0;
+            } else {
+                a.status[c] = ok ? PGN_OK : PGN_ERR_DST_TOO_SMALL;
+                a.outSizes[c] = off;  // the reference's "Required size" on failure
+            }
+            if (a.stats) {
+                for (int s = 0; s < kStreams; s++) {
+                    a.stats[c * PGN_STATS_PER_CHUNK + s] = s < nu ? sz[s] : 0;
+                    a.stats[c * PGN_STATS_PER_CHUNK + 5 + s] = s < nu ? fs[s] : 0;
+                }
+            }
+        }
+        wave_sync();
+    }
+    if (lane == 0) a.epochs[blockIdx.x] = epoch;
+    P.flush();
+}
+
+template <int Codec>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void dec_chunk_kernel(DecArgs a)
+{
+    const int lane = lane_id();
+    const DecLayout lay = dec_layout();
+    uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
+    DecScratch S;
+    S.lit = sbase + lay.lit;
+    S.seqs = (uint32_t*)(sbase + lay.seqs);
+    S.maxSeq = kMaxDecSeq;
+    S.tables = (uint32_t*)(sbase + lay.tables);
+    S.htab = (uint16_t*)(sbase + lay.htab);
+    uint8_t* inter = sbase + lay.bytes;
+    PhaseProf P;
+    P.init(a.prof);
+    while (true) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(a.queue, 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= a.nchunks) break;
+        const size_t c = u;
+        const uint32_t n = a.sampleCounts[c];
+        const uint64_t src0 = a.inOffsets[c], len = a.inSizes[c];
+        int st = PGN_OK;
+        if (Codec == kCodecVbz) {
+            // ZSTD_getFrameContentSize, then ZSTD_decompress into content + 16 padding bytes, then
+            // svb16::decode and "consumed + padding == size" (signal_compression.cpp:100-131)
+            bool fok = false;
+            const uint64_t cs = z1::frame_content_size(a.in + src0, (size_t)len, &fok);
+            if (!fok) st = PGN_ERR_NOT_ZSTD;
+            else if (cs + kVbzPadding > kInterCap || len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
+            else {
+                const long r = zstd_decompress_wave(a.in + src0, (size_t)len, inter, (size_t)cs + kVbzPadding, S, P);
+                wave_sync();
+                if (r < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
+                else {
+                    const uint64_t total = cs + kVbzPadding;
+                    if (svb_key_length(n) > cs) {
+                        st = svb_key_length(n) <= total ? PGN_ERR_REMAINING : PGN_ERR_CORRUPT;
+                    } else {
+                        const MergeOut mo = vbz_merge_chunk(inter, total, a.samples + a.sampleOffsets[c], n);
+                        if (mo.bad) st = PGN_ERR_CORRUPT;
+                        else if (mo.consumed != cs) st = PGN_ERR_REMAINING;
+                    }
+                }
+            }
+        } else {
+            DecUnit d[kStreams];
+            st = c5_parse_chunk(a.in, src0, len, d);  // C5.hpp:477-586
+            st = __builtin_amdgcn_readfirstlane(st);
+            uint64_t total = 0;
+            if (st == PGN_OK) {
+#pragma unroll
+                for (int s = 0; s < kStreams; s++) {  // C5.hpp:588-667, in blob order
+                    if (st == PGN_OK) {
+                        const long r = zstd_decompress_wave(a.in + d[s].src, d[s].len, inter + d[s].interOff, d[s].cs, S, P);
+                        wave_sync();
+                        if (r < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
+                        d[s].dres = (int32_t)r;
+                        total += d[s].cs;
+                    }
+                }
+            }
+            if (st == PGN_OK) {
+                const MergeOut mo = c5_merge_chunk(inter, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres, (uint64_t)d[3].dres,
+                                                   a.samples + a.sampleOffsets[c], n);
+                if (mo.bad) st = PGN_ERR_CORRUPT;
+                else if (mo.consumed != total) st = PGN_ERR_REMAINING;
+            }
+        }
+        P.mark(6);
+        if (lane == 0) a.status[c] = st;
+        wave_sync();
+    }
     P.flush();
 }
 
@@ -581,7 +833,11 @@ struct pgn_ctx {
     hipStream_t stream = nullptr;
     int numCUs = 0;
     size_t encSlotsMax = 0, decSlotsMax = 0;
-    size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH)
+    // pipeline per direction: the fused per-chunk kernel, or the three-kernel sub-batch pipeline
+    // ("staged"); PGN_ENC_PIPELINE / PGN_DEC_PIPELINE = fused | staged override the measured defaults
+    bool encStaged = false, decStaged = true;
+    size_t encFusedSlotsMax = 0, decFusedSlotsMax = 0;
+    size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH, staged pipeline)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
@@ -666,6 +922,15 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     int encPerCU = 0, decPerCU = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&encPerCU, enc_zstd_kernel, 64, 0));
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&decPerCU, dec_zstd_kernel, 64, 0));
+    int fe = 0, fd = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&fe, enc_chunk_kernel<kCodecC5>, 64, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&fd, dec_chunk_kernel<kCodecC5>, 64, 0));
+    if (fe < 1) fe = 1;
+    if (fd < 1) fd = 1;
+    if (const char* v = getenv("PGN_ENC_WG_PER_CU")) { const int x = atoi(v); if (x > 0 && x < fe) fe = x; }
+    if (const char* v = getenv("PGN_DEC_WG_PER_CU")) { const int x = atoi(v); if (x > 0 && x < fd) fd = x; }
+    c->encFusedSlotsMax = (size_t)c->numCUs * (size_t)(fe > 32 ? 32 : fe);
+    c->decFusedSlotsMax = (size_t)c->numCUs * (size_t)(fd > 32 ? 32 : fd);
     if (encPerCU < 1) encPerCU = 1;
     if (decPerCU < 1) decPerCU = 1;
     // resident zstd workgroups per CU (tuning knobs PGN_ENC_WG_PER_CU / PGN_DEC_WG_PER_CU: fewer
@@ -674,6 +939,8 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     if (const char* v = getenv("PGN_DEC_WG_PER_CU")) { const int x = atoi(v); if (x > 0 && x < decPerCU) decPerCU = x; }
     c->encSlotsMax = (size_t)c->numCUs * (size_t)(encPerCU > 32 ? 32 : encPerCU);
     c->decSlotsMax = (size_t)c->numCUs * (size_t)(decPerCU > 32 ? 32 : decPerCU);
+    if (const char* pp = getenv("PGN_ENC_PIPELINE")) c->encStaged = strcmp(pp, "staged") == 0;
+    if (const char* pp = getenv("PGN_DEC_PIPELINE")) c->decStaged = strcmp(pp, "staged") == 0;
     if (const char* sb = getenv("PGN_SUBBATCH")) {
         long v = atol(sb);
         if (v > 0) c->subBatch = (size_t)v;
@@ -734,7 +1001,7 @@ static int ensure_enc(pgn_ctx* c, size_t slots, size_t G)
         (void)hipFree(c->epochs);
         c->encScratch = nullptr;
         c->epochs = nullptr;
-        const size_t sb = enc_layout().bytes;
+        const size_t sb = enc_slot_bytes();
         HIPCHK(hipMalloc(&c->encScratch, sb * slots));
         HIPCHK(hipMalloc(&c->epochs, 4 * slots));
         // tag 0 never matches: a zeroed table is an empty table for every epoch >= 1.  The context
@@ -760,7 +1027,7 @@ static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
         (void)hipStreamSynchronize(c->stream);
         (void)hipFree(c->decScratch);
         c->decScratch = nullptr;
-        HIPCHK(hipMalloc(&c->decScratch, dec_layout().bytes * slots));
+        HIPCHK(hipMalloc(&c->decScratch, dec_slot_bytes() * slots));
         c->decSlots = slots;
     }
     if (G > c->decG) {  // G = chunk capacity over all buffers
@@ -788,6 +1055,73 @@ static int ensure_queues(pgn_ctx* c, size_t n, hipStream_t s)
     return PGN_OK;
 }
 
+static int launch_encode_fused(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples,
+                               const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, uint8_t* d_out,
+                               const uint64_t* d_out_offsets, const uint64_t* d_out_caps, uint64_t* d_out_sizes,
+                               int32_t* d_status, uint64_t* d_stats, hipStream_t s)
+{
+    const size_t slots = nchunks < c->encFusedSlotsMax ? nchunks : c->encFusedSlotsMax;
+    int rc = ensure_enc(c, slots, 0);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    rc = ensure_queues(c, 1, s);
+    if (rc) return rc;
+    EncArgs a{};
+    a.nchunks = nchunks;
+    a.samples = d_samples;
+    a.sampleOffsets = d_sample_offsets;
+    a.sampleCounts = d_sample_counts;
+    a.out = d_out;
+    a.outOffsets = d_out_offsets;
+    a.outCaps = d_out_caps;
+    a.outSizes = d_out_sizes;
+    a.status = d_status;
+    a.stats = d_stats;
+    a.slotScratch = c->encScratch;
+    a.slotBytes = enc_slot_bytes();
+    a.epochs = c->epochs;
+    a.prof = c->prof;
+    a.queue = c->queues;
+    if (codec == kCodecVbz) hipLaunchKernelGGL(enc_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(enc_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    c->encTimed = true;
+    return PGN_OK;
+}
+
+static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                               const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
+                               const uint32_t* d_sample_counts, int32_t* d_status, hipStream_t s)
+{
+    const size_t slots = nchunks < c->decFusedSlotsMax ? nchunks : c->decFusedSlotsMax;
+    int rc = ensure_dec(c, slots, 0);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    rc = ensure_queues(c, 1, s);
+    if (rc) return rc;
+    DecArgs a{};
+    a.nchunks = nchunks;
+    a.in = d_in;
+    a.inOffsets = d_in_offsets;
+    a.inSizes = d_in_sizes;
+    a.samples = d_samples;
+    a.sampleOffsets = d_sample_offsets;
+    a.sampleCounts = d_sample_counts;
+    a.status = d_status;
+    a.slotScratch = c->decScratch;
+    a.slotBytes = dec_slot_bytes();
+    a.prof = c->prof ? c->prof + kPhases : nullptr;
+    a.queue = c->queues;
+    c->lastUnits = nullptr;
+    if (codec == kCodecVbz) hipLaunchKernelGGL(dec_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(dec_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    c->decTimed = true;
+    return PGN_OK;
+}
+
 static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
                          const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
                          const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
@@ -795,6 +1129,9 @@ static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (!c->encStaged)
+        return launch_encode_fused(c, codec, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
+                                   d_out_caps, d_out_sizes, d_status, d_stats, s);
     const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
     const size_t passes = (nchunks + G - 1) / G;
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
@@ -820,7 +1157,7 @@ static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d
     a.status = d_status;
     a.stats = d_stats;
     a.slotScratch = c->encScratch;
-    a.slotBytes = enc_layout().bytes;
+    a.slotBytes = enc_slot_bytes();
     a.epochs = c->epochs;
     a.prof = c->prof;
     a.G = G;
@@ -859,6 +1196,9 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (!c->decStaged)
+        return launch_decode_fused(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                                   d_sample_counts, d_status, s);
     const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
     const size_t passes = (nchunks + G - 1) / G;
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
@@ -882,7 +1222,7 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     a.sampleCounts = d_sample_counts;
     a.status = d_status;
     a.slotScratch = c->decScratch;
-    a.slotBytes = dec_layout().bytes;
+    a.slotBytes = dec_slot_bytes();
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.G = G;
     a.nu = nu;
@@ -1013,6 +1353,14 @@ int pgn_debug_decode_units(pgn_ctx* c, void* out, size_t nchunks)
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, c->lastUnits, nchunks * kStreams * sizeof(DecUnit), hipMemcpyDeviceToHost));
     return PGN_OK;
+}
+
+const char* pgn_ctx_kernels(pgn_ctx* c, int direction)
+{
+    if (!c) return "";
+    if (direction == 0)
+        return c->encStaged ? "enc_split_kernel + enc_zstd_kernel + enc_assemble_kernel" : "enc_chunk_kernel<C5>";
+    return c->decStaged ? "dec_parse_kernel + dec_zstd_kernel + dec_merge_kernel" : "dec_chunk_kernel<C5>";
 }
 
 float pgn_ctx_last_encode_ms(pgn_ctx* c)

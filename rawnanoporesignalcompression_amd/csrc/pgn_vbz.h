@@ -144,9 +144,8 @@ __device__ __forceinline__ void vbz_merge_step(const VbzMergeLds& W, uint32_t kw
 }
 
 __device__ __forceinline__ int vbz_merge_wave(const uint8_t* __restrict__ in, uint64_t total, int16_t* __restrict__ out,
-                                              uint32_t n, uint64_t* consumed)
+                                              uint32_t n, uint64_t* consumed, VbzMergeLds& W)
 {
-    __shared__ VbzMergeLds W;
     const uint32_t lane = (uint32_t)lane_id();
     if (n == 0) {
         *consumed = 0;

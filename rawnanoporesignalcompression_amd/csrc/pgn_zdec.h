@@ -23,7 +23,7 @@ constexpr unsigned kHufLdsLog = 11;  // Huffman tables up to this log live in LD
 // Per-workgroup LDS, sized for four decode waves per SIMD: the literal stage (table, boundary
 // bitmap, staging rows) and the sequences stage overlay each other.  A Huffman table that must
 // outlive a sequences stage (treeless literals in a later block) is parked in HBM (DecScratch::htab).
-struct DecLds {
+struct alignas(16) DecLds {
     union {
         struct {  // literals stage
             uint16_t tab[1u << kHufLdsLog];   // Huffman decode table: symbol | nbBits << 8

@@ -27,7 +27,7 @@ struct WCTable {
 
 // LDS of one encode wave.  The match search and the literal stage never overlap, so their
 // workspaces share storage.
-struct EncLds {
+struct alignas(16) EncLds {
     union {
         struct {  // match search: hash-slot filter of the current round (bit per lane), the round's visits
             uint64_t filt[kFiltSlots];
