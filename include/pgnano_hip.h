@@ -117,6 +117,43 @@ int pgn_vbz_decompress_batch_device(pgn_ctx *ctx, size_t nchunks, const uint8_t 
                                     const uint64_t *d_in_sizes, int16_t *d_samples, const uint64_t *d_sample_offsets,
                                     const uint32_t *d_sample_counts, int32_t *d_status, void *stream);
 
+/* ---- The other compile-time pgnano variants as a runtime choice ------------------------------
+ * The reference builds one binary per `#define COMPRESSOR_*` (pgnano.cpp:1, 70-92, 105-125;
+ * utils/compile_all.sh); blobs carry no variant tag, so reader and writer must agree on it.  Same
+ * conventions as the C5 entry points (destination capacity max(2n+26, 1024) from
+ * pgn_compressed_signal_max_size; C5 through these calls equals the C5 functions above).
+ *   C4   compress_signal_N02    (pgnano/svb16/C4.hpp:274-679)    5 frames, C5 layout on raw values
+ *   C1   compress_signal_KD     (C1.hpp:202-382)                 2 frames: svb16 keys, svb16 data
+ *   C2   compress_signal_lh     (C2.hpp:195-463)                 3 frames: keys, low bytes, high bytes
+ *   C3   compress_signal_ll_lh  (C3.hpp:212-503)                 4 frames: keys, small low, big low, big high
+ *   VBZ0 compress_signal_VBZ1   (VBZ_0.hpp:316-423)              1 frame: 2-bit keys + nibble stream
+ * VBZ0 compresses straight into the destination ("Failed to compress data" = PGN_ERR_ZSTD_COMPRESS
+ * when the frame does not fit); C1/C2/C3 copy into it unchecked in the reference, here a
+ * too-small destination is PGN_ERR_DST_TOO_SMALL with the required size, as for C5/C4.  Streams
+ * above one zstd block (128 KiB) return PGN_ERR_UNSUPPORTED. */
+typedef enum pgn_variant {
+    PGN_VARIANT_C5 = 0,
+    PGN_VARIANT_C4 = 1,
+    PGN_VARIANT_C1 = 2,
+    PGN_VARIANT_C2 = 3,
+    PGN_VARIANT_C3 = 4,
+    PGN_VARIANT_VBZ0 = 5
+} pgn_variant;
+
+int pgn_variant_compress_signal(pgn_ctx *ctx, int variant, const int16_t *samples, size_t sample_count, uint8_t *dst,
+                                size_t dst_capacity, size_t *out_size);
+int pgn_variant_decompress_signal(pgn_ctx *ctx, int variant, const uint8_t *compressed, size_t compressed_size,
+                                  int16_t *dst, size_t sample_count);
+/* d_stats: raw stream sizes at [0..frames), frame sizes at [5..5+frames), in frame order */
+int pgn_variant_compress_batch_device(pgn_ctx *ctx, int variant, size_t nchunks, const int16_t *d_samples,
+                                      const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts,
+                                      uint8_t *d_out, const uint64_t *d_out_offsets, const uint64_t *d_out_caps,
+                                      uint64_t *d_out_sizes, int32_t *d_status, uint64_t *d_stats, void *stream);
+int pgn_variant_decompress_batch_device(pgn_ctx *ctx, int variant, size_t nchunks, const uint8_t *d_in,
+                                        const uint64_t *d_in_offsets, const uint64_t *d_in_sizes, int16_t *d_samples,
+                                        const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts,
+                                        int32_t *d_status, void *stream);
+
 /* Device generator of the synthetic nanopore-like reads used by bench.py (integer-only, identical
  * to the checker's pgno_synth_read): global read first_read + r * read_stride ->
  * d_samples[d_sample_offsets[r] .. + d_sample_counts[r]). */

@@ -456,6 +456,406 @@ int pgno_vbz_decompress(const uint8_t *src, size_t len, int16_t *out, uint32_t n
 }
 
 /* ----------------------------------------------------------------------------------------------
+ * The other compile-time variants of pgnano.cpp:70-92 / 105-125 (utils/compile_all.sh builds one
+ * binary per #define COMPRESSOR_*), selected here by a runtime id:
+ *   C4   compress_signal_N02   C4.hpp:53-249, 274-470 / 473-679: C5's layout, classes on raw values
+ *   C1   compress_signal_KD    C1.hpp:57-194, 202-285 / 289-382: svb16 keys | data, two frames
+ *   C2   compress_signal_lh    C2.hpp:52-189, 195-316 / 318-463: keys, every low byte, big high bytes
+ *   C3   compress_signal_ll_lh C3.hpp:53-206, 212-354 / 356-503: keys, small low, big low, big high
+ *   VBZ0 compress_signal_VBZ1  VBZ_0.hpp:60-307, 316-362 / 364-423: 2-bit keys + nibble data, one
+ *        frame compressed straight into the destination span
+ * A blob is frames 1..nf-1 each behind a u64 length prefix, then the last frame (implicit length).
+ * The pgnano svb16 decoders need no padding (pgnano/svb16/decode.hpp:16-23), so a decode must
+ * consume exactly the sum of the frame content sizes.  C1/C2/C3 memcpy into the destination without
+ * a capacity check (UB when it is too small); here that is PGNO_ERR_DST_TOO_SMALL with the required
+ * size, as C5/C4 report it.
+ * -------------------------------------------------------------------------------------------- */
+enum { PGNO_V_C5 = 0, PGNO_V_C4 = 1, PGNO_V_C1 = 2, PGNO_V_C2 = 3, PGNO_V_C3 = 4, PGNO_V_VBZ0 = 5 };
+
+static size_t key1_len(uint32_t n) { return ((size_t)n >> 3) + ((((size_t)n & 7u) + 7u) >> 3); } /* svb16_key_length */
+static size_t key2_len(uint32_t n) { return ((size_t)n + 3u) / 4u; }                             /* svb16_key_length_2bit */
+
+/* C4 split (encode_scalar_N02, C4.hpp:53-145): v==0 -> 0; v<16 -> nibble v; v<256 -> byte v; else L */
+static void c4_split(const int16_t *x, uint32_t n, uint8_t *const st[5], uint64_t sz[5])
+{
+    for (int i = 0; i < 5; i++) sz[i] = 0;
+    if (n == 0) return;
+    uint64_t nk = key2_len(n), ns = 0, nm = 0, nl = 0;
+    memset(st[0], 0, nk);
+    uint16_t prev = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint16_t cur = (uint16_t)x[i];
+        uint16_t v = zz_enc((uint16_t)(cur - prev));
+        prev = cur;
+        unsigned code;
+        if (v == 0) {
+            code = 0;
+        } else if (v < 16) {
+            code = 1;
+            if ((ns & 1u) == 0) st[1][ns >> 1] = (uint8_t)v;
+            else st[1][ns >> 1] |= (uint8_t)(v << 4);
+            ns++;
+        } else if (v < 256) {
+            code = 2;
+            st[2][nm++] = (uint8_t)v;
+        } else {
+            code = 3;
+            st[3][nl] = (uint8_t)(v & 0xFFu);
+            st[4][nl] = (uint8_t)(v >> 8);
+            nl++;
+        }
+        st[0][i >> 2] |= (uint8_t)(code << (2u * (i & 3u)));
+    }
+    sz[0] = nk; sz[1] = (ns + 1) / 2; sz[2] = nm; sz[3] = nl; sz[4] = nl;
+}
+
+/* C4 merge (decode_scalar_N02, C4.hpp:166-249): C5's walk without the class offsets */
+static int c4_merge(const uint8_t *inter, uint64_t total, uint64_t dS, uint64_t dM, uint64_t dLl,
+                    int16_t *out, uint32_t n, uint64_t *consumed)
+{
+    uint64_t kl = key2_len(n);
+    uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
+    if (n == 0) { *consumed = ph; return PGNO_OK; }
+    uint64_t sn = 0;
+    uint16_t prev = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t kb = i >> 2;
+        if (kb >= total) return PGNO_ERR_CORRUPT;
+        unsigned code = (inter[kb] >> (2u * (i & 3u))) & 3u;
+        uint16_t v;
+        if (code == 0) {
+            v = 0;
+        } else if (code == 1) {
+            uint64_t b = ps + (sn >> 1);
+            if (b >= total) return PGNO_ERR_CORRUPT;
+            v = (uint16_t)((sn & 1u) ? (inter[b] >> 4) : (inter[b] & 0xFu));
+            sn++;
+        } else if (code == 2) {
+            if (pm >= total) return PGNO_ERR_CORRUPT;
+            v = inter[pm++];
+        } else {
+            if (pl >= total || ph >= total) return PGNO_ERR_CORRUPT;
+            v = (uint16_t)(((unsigned)inter[ph++] << 8) + inter[pl++]);
+        }
+        prev = (uint16_t)(zz_dec(v) + prev);
+        out[i] = (int16_t)prev;
+    }
+    *consumed = ph;
+    return PGNO_OK;
+}
+
+/* C2 split (encode_scalar_lh, C2.hpp:52-109): keys 1 bit (v >= 256); low byte of every sample; high
+ * byte of the big ones.  C3 split (encode_scalar_ll_lh, C3.hpp:53-110): low byte of small samples;
+ * low and high bytes of big ones. */
+static void c23_split(const int16_t *x, uint32_t n, uint8_t *const st[5], uint64_t sz[5], int c3)
+{
+    for (int i = 0; i < 5; i++) sz[i] = 0;
+    if (n == 0) return;
+    uint64_t nk = key1_len(n), a = 0, b = 0;
+    memset(st[0], 0, nk);
+    uint16_t prev = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint16_t cur = (uint16_t)x[i];
+        uint16_t v = zz_enc((uint16_t)(cur - prev));
+        prev = cur;
+        int big = v >= 256;
+        if (c3) {
+            if (big) { st[2][b] = (uint8_t)v; st[3][b] = (uint8_t)(v >> 8); b++; }
+            else st[1][a++] = (uint8_t)v;
+        } else {
+            st[1][a++] = (uint8_t)v;
+            if (big) st[2][b++] = (uint8_t)(v >> 8);
+        }
+        if (big) st[0][i >> 3] |= (uint8_t)(1u << (i & 7u));
+    }
+    sz[0] = nk; sz[1] = a; sz[2] = b; sz[3] = c3 ? b : 0;
+}
+
+/* C2 merge (decode_scalar_lh, C2.hpp:121-189): low bytes from keys_length, high bytes from
+ * keys_length + dLow; consumed = one past the last high byte.  C3 merge (decode_scalar_ll_lh,
+ * C3.hpp:130-206): small low bytes from keys_length, big low from + dLL, big high from + dLL + dLH. */
+static int c23_merge(const uint8_t *inter, uint64_t total, uint64_t d1, uint64_t d2, int16_t *out, uint32_t n,
+                     uint64_t *consumed, int c3)
+{
+    uint64_t kl = key1_len(n);
+    if (n == 0) { *consumed = kl; return PGNO_OK; }
+    uint64_t pa = kl, pb = kl + d1, ph = c3 ? kl + d1 + d2 : kl + d1;
+    uint16_t prev = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t kb = i >> 3;
+        if (kb >= total) return PGNO_ERR_CORRUPT;
+        int big = (inter[kb] >> (i & 7u)) & 1u;
+        uint16_t v;
+        if (c3) {
+            if (big) {
+                if (pb >= total || ph >= total) return PGNO_ERR_CORRUPT;
+                v = (uint16_t)(inter[pb++] | ((uint16_t)inter[ph++] << 8));
+            } else {
+                if (pa >= total) return PGNO_ERR_CORRUPT;
+                v = inter[pa++];
+            }
+        } else {
+            if (pa >= total) return PGNO_ERR_CORRUPT;
+            v = inter[pa++];
+            if (big) {
+                if (ph >= total) return PGNO_ERR_CORRUPT;
+                v |= (uint16_t)((uint16_t)inter[ph++] << 8);
+            }
+        }
+        prev = (uint16_t)(zz_dec(v) + prev);
+        out[i] = (int16_t)prev;
+    }
+    *consumed = ph;
+    return PGNO_OK;
+}
+
+/* C1 merge (decode_scalar_KD, C1.hpp:140-179): svb16 data from keys_length, 1 or 2 bytes per sample */
+static int c1_merge(const uint8_t *inter, uint64_t total, int16_t *out, uint32_t n, uint64_t *consumed)
+{
+    uint64_t p = key1_len(n);
+    if (n == 0) { *consumed = p; return PGNO_OK; }
+    uint16_t prev = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if ((i >> 3) >= total) return PGNO_ERR_CORRUPT;
+        int big = (inter[i >> 3] >> (i & 7u)) & 1u;
+        uint16_t v;
+        if (!big) {
+            if (p >= total) return PGNO_ERR_CORRUPT;
+            v = inter[p++];
+        } else {
+            if (p + 1 >= total) return PGNO_ERR_CORRUPT;
+            v = (uint16_t)(inter[p] | ((uint16_t)inter[p + 1] << 8));
+            p += 2;
+        }
+        prev = (uint16_t)(zz_dec(v) + prev);
+        out[i] = (int16_t)prev;
+    }
+    *consumed = p;
+    return PGNO_OK;
+}
+
+/* VBZ0 encode (encode_scalar_VBZ1, VBZ_0.hpp:60-172): C5's classes and offsets; the value goes to
+ * one nibble stream, 1 / 2 / 4 nibbles low first.  Returns keys + data bytes. */
+size_t pgno_vbz0_encode(const int16_t *x, uint32_t n, uint8_t *out)
+{
+    if (n == 0) return 0;
+    size_t nk = key2_len(n);
+    memset(out, 0, nk);
+    uint8_t *d = out + nk;
+    uint64_t nib = 0;
+    uint16_t prev = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint16_t cur = (uint16_t)x[i];
+        uint16_t v = zz_enc((uint16_t)(cur - prev));
+        prev = cur;
+        unsigned code, cnt;
+        if (v == 0) { code = 0; cnt = 0; }
+        else if (v <= 16) { code = 1; cnt = 1; v = (uint16_t)(v - 1); }
+        else if (v <= 272) { code = 2; cnt = 2; v = (uint16_t)(v - 17); }
+        else { code = 3; cnt = 4; v = (uint16_t)(v - 273); }
+        for (unsigned k = 0; k < cnt; k++, nib++) {
+            unsigned q = (v >> (4 * k)) & 0xFu;
+            if ((nib & 1u) == 0) d[nib >> 1] = (uint8_t)q;
+            else d[nib >> 1] |= (uint8_t)(q << 4);
+        }
+        out[i >> 2] |= (uint8_t)(code << (2u * (i & 3u)));
+    }
+    return nk + (size_t)((nib + 1) / 2);
+}
+
+/* VBZ0 decode (decode_scalar_VBZ1, VBZ_0.hpp:185-290) */
+static int vbz0_merge(const uint8_t *inter, uint64_t total, int16_t *out, uint32_t n, uint64_t *consumed)
+{
+    uint64_t kl = key2_len(n), nib = 0;
+    if (n == 0) { *consumed = 0; return PGNO_OK; } /* decode_scalar_VBZ1 returns data_span.begin() */
+    uint16_t prev = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if ((i >> 2) >= total) return PGNO_ERR_CORRUPT;
+        unsigned code = (inter[i >> 2] >> (2u * (i & 3u))) & 3u;
+        unsigned cnt = code == 0 ? 0 : (code == 1 ? 1 : (code == 2 ? 2 : 4));
+        uint16_t v = 0;
+        for (unsigned k = 0; k < cnt; k++, nib++) {
+            uint64_t b = kl + (nib >> 1);
+            if (b >= total) return PGNO_ERR_CORRUPT;
+            v |= (uint16_t)(((nib & 1u) ? (inter[b] >> 4) : (inter[b] & 0xFu)) << (4 * k));
+        }
+        v = (uint16_t)(v + (code == 0 ? 0 : (code == 1 ? 1 : (code == 2 ? 17 : 273))));
+        if (code == 0) v = 0;
+        prev = (uint16_t)(zz_dec(v) + prev);
+        out[i] = (int16_t)prev;
+    }
+    *consumed = kl + (nib + 1) / 2;
+    return PGNO_OK;
+}
+
+/* nf frames behind nf-1 u64 length prefixes (the C5 assembly, C5.hpp:409-462, with nf frames) */
+static int frames_compress(uint8_t *const st[5], const uint64_t sz[5], int nf, uint8_t *dst, size_t cap,
+                           size_t *out_len, uint64_t *stream_sizes)
+{
+    size_t fb[5], fsz[5] = {0, 0, 0, 0, 0}, ftot = 0;
+    for (int s = 0; s < nf; s++) { fb[s] = Z.bound(sz[s]); ftot += fb[s]; }
+    uint8_t *fbuf = scratch(1, ftot + 16);
+    if (!fbuf) return PGNO_ERR_ALLOC;
+    uint8_t *fr[5];
+    for (int s = 0, o = 0; s < nf; s++) { fr[s] = fbuf + o; o += (int)fb[s]; }
+    for (int s = 0; s < nf; s++) {
+        size_t r = Z.compress(fr[s], fb[s], st[s], sz[s], 1);
+        if (Z.iserror(r)) return PGNO_ERR_ZSTD_COMPRESS;
+        fsz[s] = r;
+    }
+    size_t total = 8 * (size_t)(nf - 1);
+    for (int s = 0; s < nf; s++) total += fsz[s];
+    if (stream_sizes) {
+        for (int s = 0; s < 5; s++) {
+            stream_sizes[s] = s < nf ? sz[s] : 0;
+            stream_sizes[5 + s] = s < nf ? fsz[s] : 0;
+        }
+    }
+    *out_len = total;
+    if (cap < total) return PGNO_ERR_DST_TOO_SMALL;
+    uint8_t *p = dst;
+    for (int s = 0; s < nf; s++) {
+        if (s < nf - 1) { put_u64(p, (uint64_t)fsz[s]); p += 8; }
+        memcpy(p, fr[s], fsz[s]);
+        p += fsz[s];
+    }
+    return PGNO_OK;
+}
+
+/* parse + ZSTD_decompress of nf frames into one intermediate (the decompress_signal_* front half) */
+static int frames_decompress(const uint8_t *src, size_t len, int nf, uint8_t **inter_out, uint64_t *total_out,
+                             uint64_t dres[5])
+{
+    const uint8_t *fp[5];
+    uint64_t fl[5];
+    unsigned long long cs[5];
+    size_t pos = 0;
+    for (int s = 0; s < nf; s++) {
+        if (s < nf - 1) {
+            if (pos > len || len - pos < 8) return PGNO_ERR_CORRUPT;
+            fl[s] = get_u64(src + pos);
+            pos += 8;
+            if (fl[s] > len - pos) return PGNO_ERR_CORRUPT;
+        } else {
+            fl[s] = len - pos;
+        }
+        fp[s] = src + pos;
+        cs[s] = Z.fcs(fp[s], (size_t)fl[s]);
+        if (Z.iserror((size_t)cs[s])) return PGNO_ERR_NOT_ZSTD;
+        pos += (size_t)fl[s];
+    }
+    uint64_t total = 0;
+    for (int s = 0; s < nf; s++) total += cs[s];
+    if (total > ((uint64_t)1 << 40)) return PGNO_ERR_ALLOC;
+    uint8_t *inter = scratch(0, total ? total : 1);
+    if (!inter) return PGNO_ERR_ALLOC;
+    uint64_t off = 0;
+    for (int s = 0; s < nf; s++) {
+        size_t r = Z.decompress(inter + off, (size_t)cs[s], fp[s], (size_t)fl[s]);
+        if (Z.iserror(r)) return PGNO_ERR_ZSTD_DECOMPRESS;
+        dres[s] = r;
+        off += cs[s];
+    }
+    *inter_out = inter;
+    *total_out = total;
+    return PGNO_OK;
+}
+
+/* stream_sizes (optional, 10 entries): raw stream sizes then frame sizes, as pgno_c5_compress */
+int pgno_variant_compress(int variant, const int16_t *x, uint32_t n, uint8_t *dst, size_t cap, size_t *out_len,
+                          uint64_t *stream_sizes)
+{
+    if (!zok()) return PGNO_ERR_NO_ZSTD;
+    if (variant == PGNO_V_C5) return pgno_c5_compress(x, n, dst, cap, out_len, stream_sizes);
+    size_t need = key2_len(n) + 4 * (size_t)n + 64;
+    uint8_t *buf = scratch(0, 2 * need);
+    if (!buf) return PGNO_ERR_ALLOC;
+    uint8_t *st[5];
+    uint64_t sz[5] = {0, 0, 0, 0, 0};
+    int nf;
+    switch (variant) {
+    case PGNO_V_C4:
+        st[0] = buf; st[1] = st[0] + key2_len(n) + 1; st[2] = st[1] + n + 1; st[3] = st[2] + n + 1; st[4] = st[3] + n + 1;
+        c4_split(x, n, st, sz);
+        nf = 5;
+        break;
+    case PGNO_V_C1: {
+        size_t m = pgno_vbz_svb_encode(x, n, buf);
+        st[0] = buf; sz[0] = n ? key1_len(n) : 0;
+        st[1] = buf + sz[0]; sz[1] = m - sz[0];
+        nf = 2;
+        break;
+    }
+    case PGNO_V_C2:
+    case PGNO_V_C3:
+        st[0] = buf; st[1] = st[0] + key1_len(n) + 1; st[2] = st[1] + n + 1; st[3] = st[2] + n + 1; st[4] = st[3] + n + 1;
+        c23_split(x, n, st, sz, variant == PGNO_V_C3);
+        nf = variant == PGNO_V_C3 ? 4 : 3;
+        break;
+    case PGNO_V_VBZ0: {
+        size_t m = pgno_vbz0_encode(x, n, buf);
+        /* ZSTD_compress straight into the destination span (VBZ_0.hpp:345-350) */
+        size_t r = Z.compress(dst, cap, buf, m, 1);
+        if (stream_sizes) {
+            memset(stream_sizes, 0, 10 * sizeof(uint64_t));
+            stream_sizes[0] = m;
+            stream_sizes[5] = Z.iserror(r) ? 0 : r;
+        }
+        if (Z.iserror(r)) return PGNO_ERR_ZSTD_COMPRESS;
+        *out_len = r;
+        return PGNO_OK;
+    }
+    default:
+        return PGNO_ERR_ALLOC;
+    }
+    return frames_compress(st, sz, nf, dst, cap, out_len, stream_sizes);
+}
+
+int pgno_variant_decompress(int variant, const uint8_t *src, size_t len, int16_t *out, uint32_t n)
+{
+    if (!zok()) return PGNO_ERR_NO_ZSTD;
+    if (variant == PGNO_V_C5) return pgno_c5_decompress(src, len, out, n);
+    int nf = variant == PGNO_V_C4 ? 5 : (variant == PGNO_V_C1 ? 2 : (variant == PGNO_V_C2 ? 3 : (variant == PGNO_V_C3 ? 4 : 1)));
+    uint8_t *inter = NULL;
+    uint64_t total = 0, dres[5] = {0, 0, 0, 0, 0}, consumed = 0;
+    int rc = frames_decompress(src, len, nf, &inter, &total, dres);
+    if (rc != PGNO_OK) return rc;
+    switch (variant) {
+    case PGNO_V_C4: rc = c4_merge(inter, total, dres[1], dres[2], dres[3], out, n, &consumed); break;
+    case PGNO_V_C1: rc = c1_merge(inter, total, out, n, &consumed); break;
+    case PGNO_V_C2: rc = c23_merge(inter, total, dres[1], 0, out, n, &consumed, 0); break;
+    case PGNO_V_C3: rc = c23_merge(inter, total, dres[1], dres[2], out, n, &consumed, 1); break;
+    case PGNO_V_VBZ0: rc = vbz0_merge(inter, total, out, n, &consumed); break;
+    default: return PGNO_ERR_ALLOC;
+    }
+    if (rc != PGNO_OK) return rc;
+    return consumed == total ? PGNO_OK : PGNO_ERR_REMAINING;
+}
+
+/* raw streams of a variant (tests: GPU split checks, blobs from other encoder settings) */
+int pgno_variant_streams(int variant, const int16_t *x, uint32_t n, uint8_t *out, uint64_t sizes[5])
+{
+    uint8_t *st[5];
+    size_t cap = (size_t)n + 8;
+    for (int s = 0; s < 5; s++) { st[s] = out + (size_t)s * 2 * cap; sizes[s] = 0; }
+    switch (variant) {
+    case PGNO_V_C5: pgno_c5_split(x, n, st[0], st[1], st[2], st[3], st[4], sizes); return 5;
+    case PGNO_V_C4: c4_split(x, n, st, sizes); return 5;
+    case PGNO_V_C1: {
+        size_t m = pgno_vbz_svb_encode(x, n, st[0]);
+        sizes[0] = n ? key1_len(n) : 0;
+        memmove(st[1], st[0] + sizes[0], m - sizes[0]);
+        sizes[1] = m - sizes[0];
+        return 2;
+    }
+    case PGNO_V_C2: c23_split(x, n, st, sizes, 0); return 3;
+    case PGNO_V_C3: c23_split(x, n, st, sizes, 1); return 4;
+    case PGNO_V_VBZ0: sizes[0] = pgno_vbz0_encode(x, n, st[0]); return 1;
+    }
+    return 0;
+}
+
+/* ----------------------------------------------------------------------------------------------
  * Synthetic nanopore-like reads (SURVEY.md 8d generator; integer-only so the GPU replicates it).
  * Implemented identically in csrc/pgn_synth.h for the device; this copy is the checker's.
  * -------------------------------------------------------------------------------------------- */

@@ -27,6 +27,8 @@ PGN_ERR_HIP = 11
 PGN_ERR_NO_DEVICE = 12
 
 PGN_MAX_CHUNK_SAMPLES = 131072
+# pgn_variant: the reference's compile-time COMPRESSOR_* variants (pgnano.cpp:70-92)
+VARIANTS = {"C5": 0, "C4": 1, "C1": 2, "C2": 3, "C3": 4, "VBZ0": 5}
 PGN_STATS_PER_CHUNK = 10
 
 # every symbol include/pgnano_hip.h declares: (name, restype, argtypes)
@@ -50,6 +52,12 @@ SIGNATURES = [
     ("pgn_vbz_compress_batch_device", C.c_int,
      [_VP, _SZ, _VP, _U64P, _U32P, _VP, _U64P, _U64P, _U64P, _I32P, _U64P, _VP]),
     ("pgn_vbz_decompress_batch_device", C.c_int, [_VP, _SZ, _VP, _U64P, _U64P, _VP, _U64P, _U32P, _I32P, _VP]),
+    ("pgn_variant_compress_signal", C.c_int, [_VP, C.c_int, _VP, _SZ, _VP, _SZ, C.POINTER(C.c_size_t)]),
+    ("pgn_variant_decompress_signal", C.c_int, [_VP, C.c_int, _VP, _SZ, _VP, _SZ]),
+    ("pgn_variant_compress_batch_device", C.c_int,
+     [_VP, C.c_int, _SZ, _VP, _U64P, _U32P, _VP, _U64P, _U64P, _U64P, _I32P, _U64P, _VP]),
+    ("pgn_variant_decompress_batch_device", C.c_int,
+     [_VP, C.c_int, _SZ, _VP, _U64P, _U64P, _VP, _U64P, _U32P, _I32P, _VP]),
     ("pgn_synth_reads_device", C.c_int,
      [_VP, _SZ, C.c_uint64, C.c_uint64, C.c_uint64, _VP, _U64P, _U32P, C.c_uint32, C.c_int32, C.c_int32, C.c_int32,
       _VP]),

@@ -86,7 +86,12 @@ class PGNanoCodec:
 
         return torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, variant: str = "C5"):
+        """variant: the reference's compile-time COMPRESSOR_* choice (pgnano.cpp:70-92) as a runtime
+        option -- "C5" (default, the reference default), "C4", "C1", "C2", "C3", "VBZ0"."""
+        if variant not in _native.VARIANTS:
+            raise ValueError(f"unknown pgnano variant {variant!r}; one of {sorted(_native.VARIANTS)}")
+        self.variant = variant
         self._lib = _native.load()
         h = C.c_void_p()
         _check(self._lib.pgn_ctx_create(int(device), C.byref(h)), f"device {device}")
@@ -104,6 +109,17 @@ class PGNanoCodec:
         except Exception:
             pass
 
+    _VARIANT_FN = {"pgn_compress_signal": "pgn_variant_compress_signal",
+                   "pgn_decompress_signal": "pgn_variant_decompress_signal",
+                   "pgn_compress_batch_device": "pgn_variant_compress_batch_device",
+                   "pgn_decompress_batch_device": "pgn_variant_decompress_batch_device"}
+
+    def _call(self, fn: str, *args):
+        """C5 (and VBZ) through their own entry points; the other variants through pgn_variant_*."""
+        if getattr(self, "variant", "C5") != "C5" and fn in self._VARIANT_FN:
+            return getattr(self._lib, self._VARIANT_FN[fn])(self._h, _native.VARIANTS[self.variant], *args)
+        return getattr(self._lib, fn)(self._h, *args)
+
     @property
     def stream(self) -> int:
         return int(self._lib.pgn_ctx_stream(self._h) or 0)
@@ -114,8 +130,7 @@ class PGNanoCodec:
         cap = self.max_size(x.size)
         out = np.empty(cap, dtype=np.uint8)
         size = C.c_size_t(0)
-        rc = getattr(self._lib, self._fn_compress)(self._h, x.ctypes.data, x.size, out.ctypes.data, cap,
-                                                   C.byref(size))
+        rc = self._call(self._fn_compress, x.ctypes.data, x.size, out.ctypes.data, cap, C.byref(size))
         if rc == _native.PGN_ERR_DST_TOO_SMALL:
             raise PGNanoError(rc, f"Destination size: {cap}, Required size: {size.value}")
         _check(rc)
@@ -129,8 +144,8 @@ class PGNanoCodec:
             destination = np.empty(int(sample_count), dtype=np.int16)
         if destination.dtype != np.int16 or not destination.flags.c_contiguous:
             raise ValueError("destination must be a contiguous int16 array")
-        _check(getattr(self._lib, self._fn_decompress)(self._h, src.ctypes.data if src.size else 0, src.size,
-                                                       destination.ctypes.data, destination.size))
+        _check(self._call(self._fn_decompress, src.ctypes.data if src.size else 0, src.size, destination.ctypes.data,
+                          destination.size))
         return destination
 
     # ---- batched device API -----------------------------------------------------------------
@@ -163,8 +178,8 @@ class PGNanoCodec:
         sizes = torch.zeros(n, dtype=torch.int64, device=dev)
         status = torch.full((n,), -1, dtype=torch.int32, device=dev)
         stats = torch.zeros((n, _native.PGN_STATS_PER_CHUNK), dtype=torch.int64, device=dev) if with_stats else None
-        _check(getattr(self._lib, self._fn_compress_batch)(
-            self._h, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
+        _check(self._call(
+            self._fn_compress_batch, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
             _ptr(status), _ptr(stats), stream or 0))
         return EncodedBatch(out, oo, caps, sizes, status, stats)
 
@@ -186,8 +201,8 @@ class PGNanoCodec:
             total = int(counts.to(torch.int64).sum().item())
             out = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
         status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-        _check(getattr(self._lib, self._fn_decompress_batch)(
-            self._h, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
+        _check(self._call(
+            self._fn_decompress_batch, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
             _ptr(blob_sizes.to(torch.int64).contiguous()), _ptr(out), _ptr(so), _ptr(counts), _ptr(status),
             stream or 0))
         return out, so, status
@@ -236,6 +251,9 @@ class VBZCodec(PGNanoCodec):
 
     _fn_compress, _fn_decompress = "pgn_vbz_compress_signal", "pgn_vbz_decompress_signal"
     _fn_compress_batch, _fn_decompress_batch = "pgn_vbz_compress_batch_device", "pgn_vbz_decompress_batch_device"
+
+    def __init__(self, device: int = 0):
+        super().__init__(device)
 
     @staticmethod
     def max_size(sample_count: int) -> int:

@@ -81,8 +81,15 @@ __device__ __forceinline__ void nwin_flush(uint8_t* W, uint32_t& fill, uint8_t* 
     fill = tail;
 }
 
+// Class offsets: C5 (N01) stores v-1 / v-17 / v-273 (C5.hpp:105-140); C4 (N02, C4.hpp:100-133)
+// stores the raw value, classes v < 16 / v < 256 / else.
+template <bool C4> struct ClassOffsets {
+    static constexpr uint32_t o1 = C4 ? 0u : 1u, o2 = C4 ? 0u : 17u, o3 = C4 ? 0u : 273u;
+    static constexpr uint32_t t1 = C4 ? 15u : 16u, t2 = C4 ? 255u : 272u;  // class >= 2 iff v > t1, 3 iff v > t2
+};
+
 // One 1024-sample step (Full: every sample of the step exists).  Returns the lane's key word.
-template <bool Full>
+template <bool Full, bool C4 = false>
 __device__ __forceinline__ uint32_t split_step(const int16_t* __restrict__ x, uint32_t n, uint32_t t, SplitLds& W,
                                                uint32_t& fS, uint32_t& fM, uint32_t& fL, uint32_t& prevX)
 {
@@ -112,7 +119,7 @@ __device__ __forceinline__ uint32_t split_step(const int16_t* __restrict__ x, ui
         v[m] = zz_enc16((uint16_t)(xv[m] - prv));
         prv = xv[m];
         const bool valid = Full || (i0 + (uint32_t)m < n);
-        const uint32_t c = (valid && v[m] != 0) ? 1u + (v[m] > 16) + (v[m] > 272) : 0u;
+        const uint32_t c = (valid && v[m] != 0) ? 1u + (v[m] > ClassOffsets<C4>::t1) + (v[m] > ClassOffsets<C4>::t2) : 0u;
         kw |= c << (2 * m);
     }
     // places: step fills + the classes of the lanes below + my own running ranks
@@ -128,8 +135,8 @@ __device__ __forceinline__ uint32_t split_step(const int16_t* __restrict__ x, ui
 #pragma unroll
     for (int m = 0; m < 16; m++) {
         const uint32_t c = (kw >> (2 * m)) & 3u;
-        W.S[c == 1 ? qS : dS] = (uint8_t)(v[m] - 1u);
-        W.M[c == 2 ? qM : dS] = (uint8_t)(v[m] - 17u);
+        W.S[c == 1 ? qS : dS] = (uint8_t)(v[m] - ClassOffsets<C4>::o1);
+        W.M[c == 2 ? qM : dS] = (uint8_t)(v[m] - ClassOffsets<C4>::o2);
         qS += (c == 1);
         qM += (c == 2);
     }
@@ -138,7 +145,7 @@ __device__ __forceinline__ uint32_t split_step(const int16_t* __restrict__ x, ui
         for (int m = 0; m < 16; m++) {
             const uint32_t c = (kw >> (2 * m)) & 3u;
             if (c == 3) {
-                const uint32_t w = v[m] - 273u;
+                const uint32_t w = v[m] - ClassOffsets<C4>::o3;
                 W.L[qL] = (uint8_t)w;
                 W.H[qL] = (uint8_t)(w >> 8);
                 qL++;
@@ -151,7 +158,8 @@ __device__ __forceinline__ uint32_t split_step(const int16_t* __restrict__ x, ui
     return kw;
 }
 
-// sizes[5] = {keys, S, M, Llow, Lhigh} bytes.
+// sizes[5] = {keys, S, M, Llow, Lhigh} bytes.  C4: the N02 variant (same layout, raw values).
+template <bool C4 = false>
 __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uint32_t n, const C5Streams& st, uint32_t sizes[5],
                                               SplitLds& W)
 {
@@ -161,8 +169,8 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
     uint32_t prevX = 0;                       // last sample of the previous sub-step (wave-uniform)
     for (uint32_t t = 0; t < n; t += kSplitStep) {
         const bool full = t + kSplitStep <= n;
-        const uint32_t kw = full ? split_step<true>(x, n, t, W, fS, fM, fL, prevX)
-                                 : split_step<false>(x, n, t, W, fS, fM, fL, prevX);
+        const uint32_t kw = full ? split_step<true, C4>(x, n, t, W, fS, fM, fL, prevX)
+                                 : split_step<false, C4>(x, n, t, W, fS, fM, fL, prevX);
         fH = fL;
         const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
         uint8_t* kout = st.K + (t >> 2);
@@ -223,7 +231,7 @@ __device__ __forceinline__ uint64_t stage_bytes(uint8_t* W, const uint8_t* in, u
 // plus the class counts of the lanes below it (one packed DPP scan), so each lane walks its 16
 // samples alone: one LDS byte read per stream and sample, a running 16-bit sum, and a second scan
 // carries the sum across lanes.  Outputs leave as two 16-byte stores per lane.
-template <bool Full>
+template <bool Full, bool C4 = false>
 __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, bool any3, uint32_t qS, uint32_t qM, uint32_t qL,
                                            uint32_t dLH, uint32_t& carry, int16_t* __restrict__ out, uint32_t t,
                                            uint32_t n)
@@ -236,8 +244,8 @@ __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, bool 
         const uint32_t c = (kw >> (2 * m)) & 3u;
         const uint32_t sb = ((uint32_t)W.S[qS >> 1] >> (4u * (qS & 1u))) & 15u;
         const uint32_t mb = W.M[qM];
-        uint32_t v = (c == 1) ? sb + 1u : ((c == 2) ? mb + 17u : 0u);
-        if (any3 && c == 3) v = (((uint32_t)W.H[qL + dLH] << 8) | (uint32_t)W.L[qL]) + 273u;
+        uint32_t v = (c == 1) ? sb + ClassOffsets<C4>::o1 : ((c == 2) ? mb + ClassOffsets<C4>::o2 : 0u);
+        if (any3 && c == 3) v = (((uint32_t)W.H[qL + dLH] << 8) | (uint32_t)W.L[qL]) + ClassOffsets<C4>::o3;
         qS += (c == 1);
         qM += (c == 2);
         qL += (c == 3);
@@ -261,6 +269,7 @@ __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, bool 
     }
 }
 
+template <bool C4 = false>
 __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
                                              uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint64_t* consumed,
                                              MergeLds& W)
@@ -309,8 +318,8 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
         const uint32_t qM = (uint32_t)(pm + mN - wM) + (e12 >> 16);
         const uint32_t qL = (uint32_t)(pl + lN - wL) + (i3 - n3);
         const uint32_t dLH = (uint32_t)((ph - wH) - (pl - wL));  // H window offset relative to L's
-        if (full) merge_step<true>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
-        else merge_step<false>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
+        if (full) merge_step<true, C4>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
+        else merge_step<false, C4>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
         sN += ns;
         mN += nm;
         lN += nl;

@@ -14,6 +14,7 @@
 #include "../../include/pgnano_hip.h"
 #include "pgn_c5.h"
 #include "pgn_vbz.h"
+#include "pgn_variants.h"
 #include "pgn_zdec.h"
 #include "pgn_zenc.h"
 
@@ -26,7 +27,7 @@ constexpr uint32_t kMaxDecSeq = kMaxStream / 3 + 2;      // any valid block: mat
 constexpr int kStreams = 5;
 // Codecs of a batch call: the pgnano C5 variant (5 zstd frames per chunk) and the pod5 VBZ codec
 // (one zstd frame per chunk).  Both share the per-chunk buffers and the zstd kernels.
-enum Codec : int { kCodecC5 = 0, kCodecVbz = 1 };
+enum Codec : int { kCodecC5 = 0, kCodecVbz = 1, kCodecC4 = 2, kCodecC1 = 3, kCodecC2 = 4, kCodecC3 = 5, kCodecVbz0 = 6 };
 
 __host__ __device__ constexpr size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -502,18 +503,28 @@ __global__ __launch_bounds__(64) void vbz_merge_kernel(DecArgs a)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fused per-chunk pipeline (the default).  One persistent wave takes whole chunks from a queue:
-//   encode: split into its slot's stream area -> the five zstd frames written straight into the
-//           chunk's blob behind their length prefixes -> size, status, stats;
-//   decode: prefixes and frame headers -> the five frames decoded into its slot's intermediate ->
-//           merge into the samples, consumed-bytes check.
+// Fused per-chunk pipeline.  One persistent wave takes whole chunks from a queue:
+//   encode: split into its slot's stream area -> the chunk's zstd frames written straight into its
+//           blob behind their length prefixes -> size, status, stats;
+//   decode: prefixes and frame headers -> the frames decoded into its slot's intermediate -> merge
+//           into the samples, consumed-bytes check.
 // Waves in different stages share each CU (VALU-bound split/merge beside latency-bound entropy
 // coding), a chunk's streams are re-read by the wave that just wrote them, and frames are never
 // staged and copied.  The split/merge LDS overlays the zstd stage's (stages of one wave never
-// overlap in time).
+// overlap in time).  Every codec runs here; C5 and VBZ also have the staged pipeline above.
 // ---------------------------------------------------------------------------------------------
-static_assert(sizeof(SplitLds) <= sizeof(EncLds) && sizeof(VbzSplitLds) <= sizeof(EncLds), "split LDS overlay");
-static_assert(sizeof(MergeLds) <= sizeof(DecLds) && sizeof(VbzMergeLds) <= sizeof(DecLds), "merge LDS overlay");
+static_assert(sizeof(SplitLds) <= sizeof(EncLds) && sizeof(VbzSplitLds) <= sizeof(EncLds) &&
+                  sizeof(Vbz0SplitLds) <= sizeof(EncLds),
+              "split LDS overlay");
+static_assert(sizeof(MergeLds) <= sizeof(DecLds) && sizeof(VbzMergeLds) <= sizeof(DecLds) &&
+                  sizeof(Vbz0MergeLds) <= sizeof(DecLds),
+              "merge LDS overlay");
+
+// Frames per chunk: C5/C4 5, C3 4, C2 3, C1 2, VBZ/VBZ0 1 (pgnano/svb16/C*.hpp, VBZ_0.hpp)
+__host__ __device__ constexpr int codec_frames(int codec)
+{
+    return codec == kCodecC5 || codec == kCodecC4 ? 5 : (codec == kCodecC3 ? 4 : (codec == kCodecC2 ? 3 : (codec == kCodecC1 ? 2 : 1)));
+}
 
 // slot scratch of the fused kernels: the zstd scratch, then the chunk's streams (encode: + one
 // frame for a stream that may not fit the destination) or its intermediate (decode)
@@ -526,6 +537,7 @@ __host__ __device__ inline size_t dec_slot_bytes() { return dec_layout().bytes +
 struct SplitOut {
     uint32_t s[kStreams];
 };
+template <bool C4>
 __device__ __noinline__ SplitOut c5_split_chunk(const int16_t* x, uint32_t n, uint8_t* streams)
 {
     x = uni(x);
@@ -534,29 +546,59 @@ __device__ __noinline__ SplitOut c5_split_chunk(const int16_t* x, uint32_t n, ui
     C5Streams st{streams + stream_off(0), streams + stream_off(1), streams + stream_off(2), streams + stream_off(3),
                  streams + stream_off(4)};
     SplitOut o;
-    c5_split_wave(x, n, st, o.s, *reinterpret_cast<SplitLds*>(&sEnc));
+    c5_split_wave<C4>(x, n, st, o.s, *reinterpret_cast<SplitLds*>(&sEnc));
+    return o;
+}
+template <bool C3>
+__device__ __noinline__ SplitOut c23_split_chunk(const int16_t* x, uint32_t n, uint8_t* streams)
+{
+    x = uni(x);
+    n = uni(n);
+    streams = uni(streams);
+    SplitOut o;
+    c23_split_wave<C3>(x, n, streams + stream_off(0), streams + stream_off(2), streams + stream_off(3),
+                       streams + stream_off(4), o.s);
     return o;
 }
 __device__ __noinline__ uint32_t vbz_split_chunk(const int16_t* x, uint32_t n, uint8_t* out)
 {
     return vbz_split_wave(uni(x), uni(n), uni(out), *reinterpret_cast<VbzSplitLds*>(&sEnc));
 }
+__device__ __noinline__ uint32_t vbz0_split_chunk(const int16_t* x, uint32_t n, uint8_t* out)
+{
+    return vbz0_split_wave(uni(x), uni(n), uni(out), *reinterpret_cast<Vbz0SplitLds*>(&sEnc));
+}
 struct MergeOut {
     int bad;
     uint64_t consumed;
 };
+template <bool C4>
 __device__ __noinline__ MergeOut c5_merge_chunk(const uint8_t* in, uint64_t total, uint64_t dS, uint64_t dM, uint64_t dLl,
                                                 int16_t* out, uint32_t n)
 {
     MergeOut o{0, 0};
-    o.bad = c5_merge_wave(uni(in), uni(total), uni(dS), uni(dM), uni(dLl), uni(out), uni(n), &o.consumed,
-                          *reinterpret_cast<MergeLds*>(&sDec));
+    o.bad = c5_merge_wave<C4>(uni(in), uni(total), uni(dS), uni(dM), uni(dLl), uni(out), uni(n), &o.consumed,
+                              *reinterpret_cast<MergeLds*>(&sDec));
+    return o;
+}
+template <bool C3>
+__device__ __noinline__ MergeOut c23_merge_chunk(const uint8_t* in, uint64_t total, uint64_t dA, uint64_t dB, int16_t* out,
+                                                 uint32_t n)
+{
+    MergeOut o{0, 0};
+    o.bad = c23_merge_wave<C3>(uni(in), uni(total), uni(dA), uni(dB), uni(out), uni(n), &o.consumed);
     return o;
 }
 __device__ __noinline__ MergeOut vbz_merge_chunk(const uint8_t* in, uint64_t total, int16_t* out, uint32_t n)
 {
     MergeOut o{0, 0};
     o.bad = vbz_merge_wave(uni(in), uni(total), uni(out), uni(n), &o.consumed, *reinterpret_cast<VbzMergeLds*>(&sDec));
+    return o;
+}
+__device__ __noinline__ MergeOut vbz0_merge_chunk(const uint8_t* in, uint64_t total, int16_t* out, uint32_t n)
+{
+    MergeOut o{0, 0};
+    o.bad = vbz0_merge_wave(uni(in), uni(total), uni(out), uni(n), &o.consumed, *reinterpret_cast<Vbz0MergeLds*>(&sDec));
     return o;
 }
 
@@ -571,6 +613,11 @@ __device__ __forceinline__ void enc_fail_chunk(const EncArgs& a, size_t c, int s
 template <int Codec>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void enc_chunk_kernel(EncArgs a)
 {
+    constexpr int nf = codec_frames(Codec);
+    // VBZ and VBZ0 compress straight into the destination span: a frame that does not fit fails
+    // (signal_compression.cpp:57-62, VBZ_0.hpp:345-350); the multi-frame variants check the total
+    // (C5.hpp:412-427) and report the required size
+    constexpr bool oneFrame = nf == 1;
     const int lane = lane_id();
     const EncLayout lay = enc_layout();
     uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
@@ -598,45 +645,65 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
             enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
             continue;
         }
-        constexpr int nu = Codec == kCodecVbz ? 1 : kStreams;
+        const int16_t* x = a.samples + a.sampleOffsets[c];
         uint32_t sz[kStreams] = {0, 0, 0, 0, 0};
-        const uint8_t* src[kStreams];
-        if (Codec == kCodecVbz) {
-            // the data part (after the ceil(n/8) key bytes) 16-byte aligned, as in vbz_split_kernel
+        const uint8_t* src[kStreams] = {streams, streams, streams, streams, streams};
+        if (Codec == kCodecVbz || Codec == kCodecC1) {
+            // svb16 keys | data, the data part 16-byte aligned (as in vbz_split_kernel)
             const uint32_t pad = (16u - (svb_key_length(n) & 15u)) & 15u;
-            sz[0] = vbz_split_chunk(a.samples + a.sampleOffsets[c], n, streams + pad);
+            const uint32_t m = vbz_split_chunk(x, n, streams + pad);
             src[0] = streams + pad;
-            if (sz[0] > z1::kMaxSrc) {  // more than one zstd block: not on the GPU path
-                enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
-                continue;
+            if (Codec == kCodecVbz) {
+                sz[0] = m;
+            } else {  // C1: the keys frame and the data frame (C1.hpp:229-266)
+                sz[0] = n ? svb_key_length(n) : 0u;
+                sz[1] = m - sz[0];
+                src[1] = src[0] + sz[0];
             }
-        } else {
-            const SplitOut so = c5_split_chunk(a.samples + a.sampleOffsets[c], n, streams);
+        } else if (Codec == kCodecVbz0) {
+            sz[0] = vbz0_split_chunk(x, n, streams);
+        } else if (Codec == kCodecC2 || Codec == kCodecC3) {
+            const SplitOut so = c23_split_chunk<Codec == kCodecC3>(x, n, streams);
 #pragma unroll
             for (int s = 0; s < kStreams; s++) sz[s] = so.s[s];
+            src[0] = streams + stream_off(0);
+            src[1] = streams + stream_off(2);
+            src[2] = streams + stream_off(Codec == kCodecC3 ? 3 : 4);
+            src[3] = streams + stream_off(4);
+        } else {
+            const SplitOut so = c5_split_chunk<Codec == kCodecC4>(x, n, streams);
 #pragma unroll
-            for (int s = 0; s < kStreams; s++) src[s] = streams + stream_off(s);
+            for (int s = 0; s < kStreams; s++) {
+                sz[s] = so.s[s];
+                src[s] = streams + stream_off(s);
+            }
         }
 #pragma unroll
         for (int s = 0; s < kStreams; s++) sz[s] = uni(sz[s]);
+        bool big = false;  // a stream above one zstd block: not on the GPU encoder
+#pragma unroll
+        for (int s = 0; s < nf; s++) big |= sz[s] > z1::kMaxSrc;
+        if (big) {
+            enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
+            continue;
+        }
         P.mark(0);
         wave_sync();
         uint8_t* dst = a.out + a.outOffsets[c];
         const uint64_t cap = a.outCaps[c];
         uint64_t off = 0;
         bool ok = true;
-        uint32_t fs[kStreams];
+        uint32_t fs[kStreams] = {0, 0, 0, 0, 0};
 #pragma unroll
-        for (int s = 0; s < nu; s++) {
-            if (Codec != kCodecVbz && s < 4) off += 8;  // C5.hpp:429-462 length prefixes (not before Lhigh)
+        for (int s = 0; s < nf; s++) {
+            if (s < nf - 1) off += 8;  // length prefixes of all frames but the last (C5.hpp:429-462)
             if (++epoch >= 32768u) {  // tag space exhausted: clear the table once
                 for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
                 epoch = 1;
                 wave_sync();
             }
             // straight into the blob when the frame bound fits the capacity; otherwise through the
-            // slot's frame buffer (the reference compresses into its own buffers, then checks the
-            // total against the destination: C5.hpp:412-427, signal_compression.cpp:57-62)
+            // slot's frame buffer (the reference compresses into its own buffers, then checks)
             const bool direct = ok && off + frame_bound(sz[s]) <= cap;
             const size_t f = uni(zstd1_compress_wave(direct ? dst + off : fbuf, src[s], sz[s], S, epoch, P));
             wave_sync();
@@ -645,7 +712,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
                 else ok = false;
                 wave_sync();
             }
-            if (Codec != kCodecVbz && s < 4 && ok && lane == 0) {
+            if (s < nf - 1 && ok && lane == 0) {
                 const uint64_t v = f;
                 __builtin_memcpy(dst + off - 8, &v, 8);
             }
@@ -654,7 +721,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
         }
         P.mark(10);
         if (lane == 0) {
-            if (Codec == kCodecVbz) {
+            if (oneFrame) {
                 a.status[c] = ok ? PGN_OK : PGN_ERR_ZSTD_COMPRESS;
                 a.outSizes[c] = ok ? off : 0;
             } else {
@@ -663,8 +730,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
             }
             if (a.stats) {
                 for (int s = 0; s < kStreams; s++) {
-                    a.stats[c * PGN_STATS_PER_CHUNK + s] = s < nu ? sz[s] : 0;
-                    a.stats[c * PGN_STATS_PER_CHUNK + 5 + s] = s < nu ? fs[s] : 0;
+                    a.stats[c * PGN_STATS_PER_CHUNK + s] = s < nf ? sz[s] : 0;
+                    a.stats[c * PGN_STATS_PER_CHUNK + 5 + s] = s < nf ? fs[s] : 0;
                 }
             }
         }
@@ -674,9 +741,47 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
     P.flush();
 }
 
+// nf frames behind nf-1 length prefixes (the decompress_signal_* front half, C5.hpp:477-586):
+// frame records with content sizes and intermediate offsets; the frames together must fit the
+// slot's intermediate.
+template <int NF>
+__device__ inline int parse_frames(const uint8_t* in, uint64_t src0, uint64_t len, DecUnit* u, uint64_t* total)
+{
+    const uint8_t* src = in + src0;
+    uint64_t pos = 0, cs[kStreams];
+    for (int s = 0; s < NF; s++) {
+        uint64_t fl;
+        if (s < NF - 1) {
+            if (pos > len || len - pos < 8) return PGN_ERR_CORRUPT;
+            fl = ld64u(src + pos);
+            pos += 8;
+            if (fl > len - pos) return PGN_ERR_CORRUPT;
+        } else {
+            fl = len - pos;  // the last frame's length is implicit
+        }
+        bool ok = false;
+        cs[s] = z1::frame_content_size(src + pos, (size_t)fl, &ok);
+        if (!ok) return PGN_ERR_NOT_ZSTD;
+        if (fl > 0xFFFFFFFFull) return PGN_ERR_UNSUPPORTED;
+        u[s].src = src0 + pos;
+        u[s].len = (uint32_t)fl;
+        pos += fl;
+    }
+    uint64_t off = 0;
+    for (int s = 0; s < NF; s++) {
+        if (cs[s] > kInterCap - kVbzPadding - off) return PGN_ERR_UNSUPPORTED;
+        u[s].cs = (uint32_t)cs[s];
+        u[s].interOff = (uint32_t)off;
+        off += cs[s];
+    }
+    *total = off;
+    return PGN_OK;
+}
+
 template <int Codec>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void dec_chunk_kernel(DecArgs a)
 {
+    constexpr int nf = codec_frames(Codec);
     const int lane = lane_id();
     const DecLayout lay = dec_layout();
     uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
@@ -696,53 +801,55 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
         if (u >= a.nchunks) break;
         const size_t c = u;
         const uint32_t n = a.sampleCounts[c];
-        const uint64_t src0 = a.inOffsets[c], len = a.inSizes[c];
-        int st = PGN_OK;
-        if (Codec == kCodecVbz) {
-            // ZSTD_getFrameContentSize, then ZSTD_decompress into content + 16 padding bytes, then
-            // svb16::decode and "consumed + padding == size" (signal_compression.cpp:100-131)
-            bool fok = false;
-            const uint64_t cs = z1::frame_content_size(a.in + src0, (size_t)len, &fok);
-            if (!fok) st = PGN_ERR_NOT_ZSTD;
-            else if (cs + kVbzPadding > kInterCap || len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
-            else {
-                const long r = zstd_decompress_wave(a.in + src0, (size_t)len, inter, (size_t)cs + kVbzPadding, S, P);
-                wave_sync();
-                if (r < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
-                else {
-                    const uint64_t total = cs + kVbzPadding;
-                    if (svb_key_length(n) > cs) {
-                        st = svb_key_length(n) <= total ? PGN_ERR_REMAINING : PGN_ERR_CORRUPT;
-                    } else {
-                        const MergeOut mo = vbz_merge_chunk(inter, total, a.samples + a.sampleOffsets[c], n);
-                        if (mo.bad) st = PGN_ERR_CORRUPT;
-                        else if (mo.consumed != cs) st = PGN_ERR_REMAINING;
-                    }
-                }
-            }
-        } else {
-            DecUnit d[kStreams];
-            st = c5_parse_chunk(a.in, src0, len, d);  // C5.hpp:477-586
-            st = __builtin_amdgcn_readfirstlane(st);
-            uint64_t total = 0;
-            if (st == PGN_OK) {
+        int16_t* out = a.samples + a.sampleOffsets[c];
+        DecUnit d[kStreams];
+        uint64_t total = 0;
+        int st = __builtin_amdgcn_readfirstlane(parse_frames<nf>(a.in, a.inOffsets[c], a.inSizes[c], d, &total));
+        if (Codec == kCodecC5 && st == PGN_OK) {  // C5: the staged path's per-stream bound
 #pragma unroll
-                for (int s = 0; s < kStreams; s++) {  // C5.hpp:588-667, in blob order
-                    if (st == PGN_OK) {
-                        const long r = zstd_decompress_wave(a.in + d[s].src, d[s].len, inter + d[s].interOff, d[s].cs, S, P);
-                        wave_sync();
-                        if (r < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
-                        d[s].dres = (int32_t)r;
-                        total += d[s].cs;
-                    }
+            for (int s = 0; s < nf; s++)
+                if (d[s].cs > kMaxStream) st = PGN_ERR_UNSUPPORTED;
+        }
+        if (st == PGN_OK) {
+#pragma unroll
+            for (int s = 0; s < nf; s++) {  // in blob order (C5.hpp:588-667)
+                if (st == PGN_OK) {
+                    // VBZ's intermediate carries svb16's 16 padding bytes (signal_compression.cpp:112-118);
+                    // the pgnano variants decompress into exactly the content size
+                    const size_t cap = Codec == kCodecVbz ? (size_t)d[s].cs + kVbzPadding : (size_t)d[s].cs;
+                    const long r = zstd_decompress_wave(a.in + d[s].src, d[s].len, inter + d[s].interOff, cap, S, P);
+                    wave_sync();
+                    if (r < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
+                    d[s].dres = (int32_t)r;
                 }
             }
-            if (st == PGN_OK) {
-                const MergeOut mo = c5_merge_chunk(inter, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres, (uint64_t)d[3].dres,
-                                                   a.samples + a.sampleOffsets[c], n);
-                if (mo.bad) st = PGN_ERR_CORRUPT;
-                else if (mo.consumed != total) st = PGN_ERR_REMAINING;
+        }
+        if (st == PGN_OK) {
+            MergeOut mo{0, 0};
+            uint64_t want = total;  // the pgnano svb16 decoders need no padding: consume everything
+            if (Codec == kCodecVbz) {
+                // svb16::decode over content + 16 padding bytes, then "consumed + padding == size"
+                // (signal_compression.cpp:100-131): keys running into the padding are "Remaining data"
+                const uint64_t padded = total + kVbzPadding;
+                if (svb_key_length(n) > total) {
+                    mo.bad = svb_key_length(n) <= padded ? 2 : 1;
+                } else {
+                    mo = vbz_merge_chunk(inter, padded, out, n);
+                }
+            } else if (Codec == kCodecC1) {
+                mo = vbz_merge_chunk(inter, total, out, n);
+            } else if (Codec == kCodecVbz0) {
+                mo = vbz0_merge_chunk(inter, total, out, n);
+            } else if (Codec == kCodecC2 || Codec == kCodecC3) {
+                mo = c23_merge_chunk<Codec == kCodecC3>(inter, total, (uint64_t)d[1].dres,
+                                                        Codec == kCodecC3 ? (uint64_t)d[2].dres : 0ull, out, n);
+            } else {
+                mo = c5_merge_chunk<Codec == kCodecC4>(inter, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres,
+                                                       (uint64_t)d[3].dres, out, n);
             }
+            if (mo.bad == 2) st = PGN_ERR_REMAINING;
+            else if (mo.bad) st = PGN_ERR_CORRUPT;
+            else if (mo.consumed != want) st = PGN_ERR_REMAINING;
         }
         P.mark(6);
         if (lane == 0) a.status[c] = st;
@@ -1082,8 +1189,16 @@ static int launch_encode_fused(pgn_ctx* c, int codec, size_t nchunks, const int1
     a.epochs = c->epochs;
     a.prof = c->prof;
     a.queue = c->queues;
-    if (codec == kCodecVbz) hipLaunchKernelGGL(enc_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(enc_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a);
+    switch (codec) {
+    case kCodecC5: hipLaunchKernelGGL(enc_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecVbz: hipLaunchKernelGGL(enc_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC4: hipLaunchKernelGGL(enc_chunk_kernel<kCodecC4>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC1: hipLaunchKernelGGL(enc_chunk_kernel<kCodecC1>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC2: hipLaunchKernelGGL(enc_chunk_kernel<kCodecC2>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC3: hipLaunchKernelGGL(enc_chunk_kernel<kCodecC3>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecVbz0: hipLaunchKernelGGL(enc_chunk_kernel<kCodecVbz0>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    default: return PGN_ERR_INVALID_ARG;
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
     c->encTimed = true;
@@ -1114,8 +1229,16 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.queue = c->queues;
     c->lastUnits = nullptr;
-    if (codec == kCodecVbz) hipLaunchKernelGGL(dec_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(dec_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a);
+    switch (codec) {
+    case kCodecC5: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecVbz: hipLaunchKernelGGL(dec_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC4: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC4>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC1: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC1>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC2: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC2>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecC3: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC3>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    case kCodecVbz0: hipLaunchKernelGGL(dec_chunk_kernel<kCodecVbz0>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
+    default: return PGN_ERR_INVALID_ARG;
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], s));
     c->decTimed = true;
@@ -1129,7 +1252,7 @@ static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (!c->encStaged)
+    if (!c->encStaged || (codec != kCodecC5 && codec != kCodecVbz))  // the other variants are fused only
         return launch_encode_fused(c, codec, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
                                    d_out_caps, d_out_sizes, d_status, d_stats, s);
     const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
@@ -1196,7 +1319,7 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (!c->decStaged)
+    if (!c->decStaged || (codec != kCodecC5 && codec != kCodecVbz))
         return launch_decode_fused(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                                    d_sample_counts, d_status, s);
     const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
@@ -1312,6 +1435,42 @@ int pgn_vbz_decompress_batch_device(pgn_ctx* c, size_t nchunks, const uint8_t* d
                                     const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
 {
     return decompress_batch(kCodecVbz, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                            d_sample_counts, d_status, stream);
+}
+
+// the pgnano variants by pgn_variant id -> internal codec
+static int variant_codec(int variant)
+{
+    switch (variant) {
+    case PGN_VARIANT_C5: return kCodecC5;
+    case PGN_VARIANT_C4: return kCodecC4;
+    case PGN_VARIANT_C1: return kCodecC1;
+    case PGN_VARIANT_C2: return kCodecC2;
+    case PGN_VARIANT_C3: return kCodecC3;
+    case PGN_VARIANT_VBZ0: return kCodecVbz0;
+    default: return -1;
+    }
+}
+
+int pgn_variant_compress_batch_device(pgn_ctx* c, int variant, size_t nchunks, const int16_t* d_samples,
+                                      const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, uint8_t* d_out,
+                                      const uint64_t* d_out_offsets, const uint64_t* d_out_caps, uint64_t* d_out_sizes,
+                                      int32_t* d_status, uint64_t* d_stats, void* stream)
+{
+    const int codec = variant_codec(variant);
+    if (codec < 0) return PGN_ERR_INVALID_ARG;
+    return compress_batch(codec, c, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
+                          d_out_caps, d_out_sizes, d_status, d_stats, stream);
+}
+
+int pgn_variant_decompress_batch_device(pgn_ctx* c, int variant, size_t nchunks, const uint8_t* d_in,
+                                        const uint64_t* d_in_offsets, const uint64_t* d_in_sizes, int16_t* d_samples,
+                                        const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts,
+                                        int32_t* d_status, void* stream)
+{
+    const int codec = variant_codec(variant);
+    if (codec < 0) return PGN_ERR_INVALID_ARG;
+    return decompress_batch(codec, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                             d_sample_counts, d_status, stream);
 }
 
@@ -1518,6 +1677,21 @@ int pgn_vbz_compress_signal(pgn_ctx* c, const int16_t* samples, size_t n, uint8_
 int pgn_vbz_decompress_signal(pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
 {
     return decompress_signal(kCodecVbz, c, src, len, dst, n);
+}
+
+int pgn_variant_compress_signal(pgn_ctx* c, int variant, const int16_t* samples, size_t n, uint8_t* dst, size_t cap,
+                                size_t* out_size)
+{
+    const int codec = variant_codec(variant);
+    if (codec < 0) return PGN_ERR_INVALID_ARG;
+    return compress_signal(codec, c, samples, n, dst, cap, out_size);
+}
+
+int pgn_variant_decompress_signal(pgn_ctx* c, int variant, const uint8_t* src, size_t len, int16_t* dst, size_t n)
+{
+    const int codec = variant_codec(variant);
+    if (codec < 0) return PGN_ERR_INVALID_ARG;
+    return decompress_signal(codec, c, src, len, dst, n);
 }
 
 static pgn_ctx* g_default = nullptr;

@@ -46,6 +46,12 @@ def oracle() -> C.CDLL:
         L.pgno_vbz_svb_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         L.pgno_vbz_bound.restype = C.c_size_t
         L.pgno_vbz_bound.argtypes = [C.c_uint32]
+        L.pgno_variant_compress.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t,
+                                            C.POINTER(C.c_size_t), C.c_void_p]
+        L.pgno_variant_decompress.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32]
+        L.pgno_variant_streams.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        L.pgno_vbz0_encode.restype = C.c_size_t
+        L.pgno_vbz0_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         L.pgno_synth_read.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint32, C.c_int32,
                                       C.c_int32, C.c_int32]
         _o = L
@@ -163,3 +169,54 @@ def synth_read(read_idx: int, n: int, seed: int = 42, p_switch_q16: int = 6554, 
     out = np.zeros(max(n, 1), np.int16)
     oracle().pgno_synth_read(seed, read_idx, n, out.ctypes.data, p_switch_q16, level_mean, level_sd, noise_sd)
     return out[:n]
+
+
+# The compile-time variants of pgnano.cpp:70-92 as runtime ids (same numbering as include/pgnano_hip.h)
+VARIANTS = {"C5": 0, "C4": 1, "C1": 2, "C2": 3, "C3": 4, "VBZ0": 5}
+VARIANT_FRAMES = {"C5": 5, "C4": 5, "C1": 2, "C2": 3, "C3": 4, "VBZ0": 1}
+
+
+def variant_compress(variant: str, x: np.ndarray, cap: int | None = None):
+    """Returns (status, blob bytes or required size, stream sizes[10])."""
+    L = oracle()
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    if cap is None:
+        cap = L.pgno_c5_bound(x.size)  # pgnano::Compressor::compressed_signal_max_size for every variant
+    out = np.zeros(max(cap, 1), np.uint8)
+    ol = C.c_size_t(0)
+    st = np.zeros(10, np.uint64)
+    rc = L.pgno_variant_compress(VARIANTS[variant], x.ctypes.data if x.size else 0, x.size, out.ctypes.data, cap,
+                                 C.byref(ol), st.ctypes.data)
+    if rc == OK:
+        return rc, out[: ol.value].tobytes(), st
+    return rc, ol.value, st
+
+
+def variant_decompress(variant: str, blob: bytes, n: int):
+    L = oracle()
+    a = _buf(blob)
+    out = np.zeros(max(n, 1), np.int16)
+    rc = L.pgno_variant_decompress(VARIANTS[variant], a.ctypes.data, len(blob), out.ctypes.data, n)
+    return rc, out[:n]
+
+
+def variant_streams(variant: str, x: np.ndarray) -> list[bytes]:
+    """The raw streams a variant hands to ZSTD_compress (one per frame)."""
+    L = oracle()
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    cap = x.size + 8
+    buf = np.zeros(10 * cap + 64, np.uint8)
+    sz = np.zeros(5, np.uint64)
+    nf = L.pgno_variant_streams(VARIANTS[variant], x.ctypes.data if x.size else 0, x.size, buf.ctypes.data,
+                                sz.ctypes.data)
+    return [buf[2 * cap * s: 2 * cap * s + int(sz[s])].tobytes() for s in range(nf)]
+
+
+def variant_assemble(frames: list[bytes]) -> bytes:
+    """nf frames, the first nf-1 behind u64 length prefixes."""
+    out = b""
+    for s, f in enumerate(frames):
+        if s < len(frames) - 1:
+            out += len(f).to_bytes(8, "little")
+        out += f
+    return out
