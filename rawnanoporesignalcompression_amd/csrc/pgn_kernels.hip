@@ -611,7 +611,7 @@ __device__ __forceinline__ void enc_fail_chunk(const EncArgs& a, size_t c, int s
 }
 
 template <int Codec>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void enc_chunk_kernel(EncArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void enc_chunk_kernel(EncArgs a)
 {
     constexpr int nf = codec_frames(Codec);
     // VBZ and VBZ0 compress straight into the destination span: a frame that does not fit fails

@@ -15,7 +15,7 @@
 namespace pgn {
 
 constexpr int kWinWords = 392;  // 1024 symbols * 12 bits / 32 + carry words
-constexpr int kFiltSlots = 1024;  // match-search round filter (64 lanes x 2 hashes)
+constexpr int kFiltSlots = 512;  // match-search round filter (64 lanes x 2 hashes)
 
 // FSE compression table of the Huffman weight alphabet (<= 13 symbols, tableLog <= 6)
 struct WCTable {
@@ -35,17 +35,18 @@ struct alignas(16) EncLds {
         };
         struct {  // literals; members grouped by lifetime so that each phase's scratch overlays the last
             uint32_t hist2[2][256];  // per-segment histograms, two 16-bit counts per word (histogram -> stream sizes)
-            union {
-                uint32_t count[256];  // histogram -> sort
-                uint32_t cw[256];     // Huffman code | nbBits << 16 (stream sizes -> encode)
-            };
             uint8_t nbBits[256];  // tree -> stream sizes
             uint16_t val[256];
             union {
                 struct {  // tree build
                     z1::HufNode nodes[2 * 256 + 4];
-                    uint16_t tanc[256];  // tree depths by pointer jumping: ancestor of internal node 256 + i
-                    uint16_t tdep[256];  //                                 distance to it
+                    union {
+                        uint32_t count[256];  // histogram -> sort (dead before the depths are computed)
+                        struct {
+                            uint16_t tanc[256];  // tree depths by pointer jumping: ancestor of internal node 256 + i
+                            uint16_t tdep[256];  //                                 distance to it
+                        };
+                    };
                     uint32_t rankLast[16];
                     uint32_t vpr[16];  // valPerRank
                 };
@@ -58,7 +59,10 @@ struct alignas(16) EncLds {
                     int16_t wnorm[16];
                     uint32_t wcumul[16];
                 };
-                uint32_t win[kWinWords];  // encode: output bit window
+                struct {  // encode (after the table description has left for HBM)
+                    uint32_t win[kWinWords];  // output bit window
+                    uint32_t cw[256];         // Huffman code | nbBits << 16 (stream sizes -> encode)
+                };
             };
         };
         struct {  // sequences section (after the literals section is written)
