@@ -5,7 +5,8 @@
 // 16 lanes per stream, in rounds.  In a round the 16 lanes of a stream take 16 consecutive windows
 // of kWinBits bits below the stream's true position T (lane j: (T - (j+1)W, T - jW]).
 //   pass A: every lane decodes its window speculatively from the window top, counting symbols and
-//           recording its codeword boundaries in the first kBmpBits bits (LDS bitmap);
+//           recording its codeword boundaries in the first kBmpBits bits (a 128-bit bitmap held
+//           in the lane's registers);
 //   sync:   the true path enters window j at lane j-1's exit; lane j walks from there until it meets
 //           one of its recorded boundaries (from there its speculative symbols are the true ones),
 //           or decodes the rest of its window itself.  A lane whose exit changed makes its successor
@@ -104,8 +105,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             sDec.stg[4 * i + 2][lane] = nx[i].z;
             sDec.stg[4 * i + 3][lane] = nx[i].w;
         }
-#pragma unroll
-        for (int w = 0; w < kBmpBits / 32; w++) sDec.bmp[w][lane] = 0;
+        uint64_t bm0 = 0, bm1 = 0;  // boundary bitmap: bit d = codeword start at hi - d (d < 128)
         const int32_t nextT = T - 16 * kWinBits;
         if (ballot(nextT > 0)) {  // next round's bytes, in flight during this one
             base = round_base(nextT - j * kWinBits);
@@ -123,7 +123,9 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 for (int u = 0; u < 2; u++) {
                     const bool act = q > lo && hi - q < kBmpBits;
                     const int32_t d = hi - q;
-                    if (act) atomicOr(&sDec.bmp[d >> 5][lane], 1u << (d & 31));
+                    const uint64_t bit = 1ull << (d & 63);
+                    bm0 |= (act && d < 64) ? bit : 0ull;
+                    bm1 |= (act && d >= 64) ? bit : 0ull;
                     const uint32_t e = stg_entry(r, lane, q - b8 - tli, tmask);
                     q = act ? q - (int32_t)(e >> 8) : q;
                     c += act ? 1u : 0u;
@@ -168,7 +170,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 stg_init(r, lane, p - b8 - tli);
                 while (p > lo) {
                     const int32_t d = hi - p;
-                    if (d < kBmpBits && ((sDec.bmp[d >> 5][lane] >> (d & 31)) & 1u)) {
+                    if (d < kBmpBits && (((d < 64 ? (bm0 >> d) : (bm1 >> (d - 64))) & 1ull) != 0)) {
                         synced = true;
                         break;
                     }
@@ -178,13 +180,10 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 }
                 if (synced) {
                     const int32_t d = hi - p;
-                    uint32_t idx = 0;
-#pragma unroll
-                    for (int ww = 0; ww < kBmpBits / 32; ww++) {
-                        const uint32_t bits = sDec.bmp[ww][lane];
-                        const int32_t rem = d - 32 * ww;
-                        idx += (uint32_t)__builtin_popcount(rem >= 32 ? bits : (rem <= 0 ? 0u : bits & ((1u << rem) - 1u)));
-                    }
+                    // boundaries recorded below d (d < 128 here)
+                    const uint64_t m0 = d >= 64 ? ~0ull : ((1ull << d) - 1ull);
+                    const uint64_t m1 = d <= 64 ? 0ull : ((1ull << (d - 64)) - 1ull);
+                    const uint32_t idx = (uint32_t)__builtin_popcountll(bm0 & m0) + (uint32_t)__builtin_popcountll(bm1 & m1);
                     cnt = w + c - idx;
                     ex = q;
                 } else {

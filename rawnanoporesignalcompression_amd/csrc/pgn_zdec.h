@@ -28,7 +28,6 @@ struct alignas(16) DecLds {
         struct {  // literals stage
             uint16_t tab[1u << kHufLdsLog];   // Huffman decode table: symbol | nbBits << 8
             // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
-            uint32_t bmp[kBmpBits / 32][64];  // speculative decode: boundary bitmap below each lane start
             uint32_t stg[kStgWords][64];      // staged stream bytes of the current round
             uint8_t wts[256];                 // weights of the current table
             uint8_t order[256];               // symbols sorted by (weight, symbol)
