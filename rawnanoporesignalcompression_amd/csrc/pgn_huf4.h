@@ -58,6 +58,22 @@ __device__ __forceinline__ uint32_t stg_entry(StgBits& r, int lane, int32_t x, u
     return sDec.tab[(uint32_t)(r.Wd >> ((x - r.wlo) & 63)) & tmask];
 }
 
+// Two decode-table entries: the codeword at x and the one below it.  One refill check and one
+// staged-word prefetch serve both lookups: refilling whenever fewer than tl bits remain above the
+// window base keeps both peeks inside the 64-bit window (x - wlo < 32 + tl after a refill, so
+// x + tl <= wlo + 54).  Halves the per-symbol refill/prefetch cost of the unpredicated loops.
+__device__ __forceinline__ void stg_entry2(StgBits& r, int lane, int32_t x, uint32_t tmask, int32_t tl, uint32_t& e1,
+                                           uint32_t& e2)
+{
+    const bool rf = x - r.wlo < tl;
+    r.Wd = rf ? ((r.Wd << 32) | r.nxw) : r.Wd;
+    r.wlo = rf ? r.wlo - 32 : r.wlo;
+    r.nxw = sDec.stg[r.wlo >= 64 ? (r.wlo >> 5) - 1 : 0][lane];
+    e1 = sDec.tab[(uint32_t)(r.Wd >> ((x - r.wlo) & 63)) & tmask];
+    const int32_t x2 = x - (int32_t)(e1 >> 8);
+    e2 = sDec.tab[(uint32_t)(r.Wd >> ((x2 - r.wlo) & 63)) & tmask];
+}
+
 // Returns false on a malformed section.
 __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
                                               PhaseProf& P)
@@ -136,9 +152,10 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 const bool act = q > lo;
                 int32_t qq = q;
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t e = stg_entry(r, lane, qq - b8 - tli, tmask);
-                    qq -= (int32_t)(e >> 8);
+                for (int u = 0; u < 2; u++) {
+                    uint32_t e1, e2;
+                    stg_entry2(r, lane, qq - b8 - tli, tmask, tli, e1, e2);
+                    qq -= (int32_t)(e1 >> 8) + (int32_t)(e2 >> 8);
                 }
                 q = act ? qq : q;
                 c += act ? 4u : 0u;
@@ -222,10 +239,11 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 if (i + 4 <= cnt) {
                     uint32_t word = 0;
 #pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
-                        p -= (int32_t)(e >> 8);
-                        word |= (e & 0xFFu) << (8 * u);
+                    for (int u = 0; u < 2; u++) {
+                        uint32_t e1, e2;
+                        stg_entry2(r, lane, p - b8 - tli, tmask, tli, e1, e2);
+                        p -= (int32_t)(e1 >> 8) + (int32_t)(e2 >> 8);
+                        word |= ((e1 & 0xFFu) | ((e2 & 0xFFu) << 8)) << (16 * u);
                     }
                     gst<uint32_t>(out + i, word);
                     i += 4;
