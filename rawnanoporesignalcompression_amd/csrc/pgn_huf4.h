@@ -135,15 +135,16 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             StgBits r;
             stg_init(r, lane, q - b8 - tli);
             while (ballot(q > lo && hi - q < kBmpBits)) {
+                uint32_t e[2];
+                stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
+                for (int u = 0; u < 2; u++) {  // the second entry is only used if the first was
                     const bool act = q > lo && hi - q < kBmpBits;
                     const int32_t d = hi - q;
                     const uint64_t bit = 1ull << (d & 63);
                     bm0 |= (act && d < 64) ? bit : 0ull;
                     bm1 |= (act && d >= 64) ? bit : 0ull;
-                    const uint32_t e = stg_entry(r, lane, q - b8 - tli, tmask);
-                    q = act ? q - (int32_t)(e >> 8) : q;
+                    q = act ? q - (int32_t)(e[u] >> 8) : q;
                     c += act ? 1u : 0u;
                 }
             }
@@ -162,11 +163,15 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             }
             while (ballot(q > lo)) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const bool act = q > lo;
-                    const uint32_t e = stg_entry(r, lane, q - b8 - tli, tmask);
-                    q = act ? q - (int32_t)(e >> 8) : q;
-                    c += act ? 1u : 0u;
+                for (int v = 0; v < 2; v++) {
+                    uint32_t e[2];
+                    stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
+#pragma unroll
+                    for (int u = 0; u < 2; u++) {
+                        const bool act = q > lo;
+                        q = act ? q - (int32_t)(e[u] >> 8) : q;
+                        c += act ? 1u : 0u;
+                    }
                 }
             }
         }
