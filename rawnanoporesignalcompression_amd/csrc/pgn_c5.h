@@ -89,15 +89,16 @@ template <bool C4> struct ClassOffsets {
 };
 
 // One 1024-sample step (Full: every sample of the step exists).  Returns the lane's key word.
+// Full steps take the lane's 32 sample bytes already loaded (a, b: prefetched one step ahead).
 template <bool Full, bool C4 = false>
-__device__ __forceinline__ uint32_t split_step(const int16_t* __restrict__ x, uint32_t n, uint32_t t, SplitLds& W,
-                                               uint32_t& fS, uint32_t& fM, uint32_t& fL, uint32_t& prevX)
+__device__ __forceinline__ uint32_t split_step(const uint4& a, const uint4& b, const int16_t* __restrict__ x, uint32_t n,
+                                               uint32_t t, SplitLds& W, uint32_t& fS, uint32_t& fM, uint32_t& fL,
+                                               uint32_t& prevX)
 {
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t i0 = t + 16u * lane;
     uint32_t xv[16];
     if (Full) {
-        const uint4 a = gld<uint4>(x + i0), b = gld<uint4>(x + i0 + 8);
         const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -167,10 +168,21 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
     uint32_t fS = 0, fM = 0, fL = 0, fH = 0;  // window fills (S in nibbles)
     uint32_t gS = 0, gM = 0, gL = 0, gH = 0;  // bytes already in HBM
     uint32_t prevX = 0;                       // last sample of the previous sub-step (wave-uniform)
+    // the samples of a full step are loaded one step ahead, so their latency overlaps a step
+    uint4 na = make_uint4(0u, 0u, 0u, 0u), nb = na;
+    if (kSplitStep <= n) {
+        na = gld<uint4>(x + 16u * lane);
+        nb = gld<uint4>(x + 16u * lane + 8);
+    }
     for (uint32_t t = 0; t < n; t += kSplitStep) {
         const bool full = t + kSplitStep <= n;
-        const uint32_t kw = full ? split_step<true, C4>(x, n, t, W, fS, fM, fL, prevX)
-                                 : split_step<false, C4>(x, n, t, W, fS, fM, fL, prevX);
+        const uint4 ca = na, cb = nb;
+        if (t + 2 * kSplitStep <= n) {
+            na = gld<uint4>(x + t + kSplitStep + 16u * lane);
+            nb = gld<uint4>(x + t + kSplitStep + 16u * lane + 8);
+        }
+        const uint32_t kw = full ? split_step<true, C4>(ca, cb, x, n, t, W, fS, fM, fL, prevX)
+                                 : split_step<false, C4>(ca, cb, x, n, t, W, fS, fM, fL, prevX);
         fH = fL;
         const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
         uint8_t* kout = st.K + (t >> 2);
