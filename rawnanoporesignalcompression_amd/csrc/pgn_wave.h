@@ -159,6 +159,14 @@ __device__ inline void wave_copy(uint8_t* dst, const uint8_t* src, size_t n)
 {
     const int lane = lane_id();
     size_t i = (size_t)lane * 16;
+    for (; i + 16 + 3 * 1024 <= n; i += 4096) {  // four 16-byte loads in flight per lane
+        const uint4 a = gld<uint4>(src + i), b = gld<uint4>(src + i + 1024), c = gld<uint4>(src + i + 2048),
+                    d = gld<uint4>(src + i + 3072);
+        gst<uint4>(dst + i, a);
+        gst<uint4>(dst + i + 1024, b);
+        gst<uint4>(dst + i + 2048, c);
+        gst<uint4>(dst + i + 3072, d);
+    }
     for (; i + 16 <= n; i += 1024) gst<uint4>(dst + i, gld<uint4>(src + i));
     for (size_t b = (n & ~(size_t)15) + (size_t)lane; b < n; b += 64) gst<uint8_t>(dst + b, gb(src + b));
 }

@@ -1155,13 +1155,20 @@ __device__ inline size_t write_raw_literals_wave(uint8_t* dst, const uint8_t* li
     return fl + n;
 }
 
+// writeRaw = false: a raw literals section is sized but not written (the caller knows it turns the
+// whole block raw and writes that instead).
 __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
-                                                PhaseProf& P)
+                                                PhaseProf& P, uint32_t writeRaw)
 {
     EncLds& L = sEnc;
     dst = uni(dst);
     lit = uni(lit);
     n = uni(n);
+    writeRaw = uni(writeRaw);
+    auto write_raw_literals_wave = [&](uint8_t* d, const uint8_t* l, uint32_t m) -> size_t {
+        if (writeRaw) return pgn::write_raw_literals_wave(d, l, m);
+        return z1::raw_lit_header_size(m) + m;
+    };
     const int lane = lane_id();
     if (n <= 63) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
     const uint32_t minGain = (n >> 6) + 2;
@@ -1350,7 +1357,9 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         P.mark(2);
     }
     uint8_t* body = dst + h + 3;
-    const size_t litSize = compress_literals_wave(body, lit, nLit, P);
+    // without sequences a raw literals section makes the block raw (lh + n + 1 >= maxCSize): it is
+    // then only sized here, and the raw block below is the one copy
+    const size_t litSize = compress_literals_wave(body, lit, nLit, P, nbSeq > 0 ? 1u : 0u);
     wave_sync();
     size_t seqSize;
     if (nbSeq == 0) {
