@@ -120,6 +120,16 @@ class PGNanoCodec:
             return getattr(self._lib, self._VARIANT_FN[fn])(self._h, _native.VARIANTS[self.variant], *args)
         return getattr(self._lib, fn)(self._h, *args)
 
+    def _launch_stream(self, stream):
+        """The HIP stream a batch call runs on (the caller's, else the context's), made to wait for
+        the caller's current stream.  The call's own allocations and fills are issued on it too, so
+        they are ordered before the kernels and the caching allocator ties them to that stream."""
+        import torch
+
+        s = torch.cuda.ExternalStream(int(stream) if stream else self.stream, device=torch.device("cuda", self.device))
+        s.wait_stream(torch.cuda.current_stream())
+        return s
+
     @property
     def stream(self) -> int:
         return int(self._lib.pgn_ctx_stream(self._h) or 0)
@@ -158,54 +168,58 @@ class PGNanoCodec:
         """
         import torch
 
-        dev = samples.device
-        n = int(sample_counts.numel())
-        counts = sample_counts.to(device=dev, dtype=torch.int32).contiguous()
-        offs = sample_offsets.to(device=dev, dtype=torch.int64).contiguous()
-        if out_caps is None:
-            caps = self._default_caps(counts)
-        else:
-            caps = out_caps.to(device=dev, dtype=torch.int64).contiguous()
-        if out_offsets is None:
-            oo = torch.zeros(n, dtype=torch.int64, device=dev)
-            if n > 1:
-                oo[1:] = torch.cumsum(caps, 0)[:-1]
-        else:
-            oo = out_offsets.to(device=dev, dtype=torch.int64).contiguous()
-        if out is None:
-            total = int((oo[-1] + caps[-1]).item()) if n else 0
-            out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
-        sizes = torch.zeros(n, dtype=torch.int64, device=dev)
-        status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-        stats = torch.zeros((n, _native.PGN_STATS_PER_CHUNK), dtype=torch.int64, device=dev) if with_stats else None
-        _check(self._call(
-            self._fn_compress_batch, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
-            _ptr(status), _ptr(stats), stream or 0))
-        return EncodedBatch(out, oo, caps, sizes, status, stats)
+        ls = self._launch_stream(stream)
+        with torch.cuda.stream(ls):
+            dev = samples.device
+            n = int(sample_counts.numel())
+            counts = sample_counts.to(device=dev, dtype=torch.int32).contiguous()
+            offs = sample_offsets.to(device=dev, dtype=torch.int64).contiguous()
+            if out_caps is None:
+                caps = self._default_caps(counts)
+            else:
+                caps = out_caps.to(device=dev, dtype=torch.int64).contiguous()
+            if out_offsets is None:
+                oo = torch.zeros(n, dtype=torch.int64, device=dev)
+                if n > 1:
+                    oo[1:] = torch.cumsum(caps, 0)[:-1]
+            else:
+                oo = out_offsets.to(device=dev, dtype=torch.int64).contiguous()
+            if out is None:
+                total = int((oo[-1] + caps[-1]).item()) if n else 0
+                out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+            sizes = torch.zeros(n, dtype=torch.int64, device=dev)
+            status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            stats = torch.zeros((n, _native.PGN_STATS_PER_CHUNK), dtype=torch.int64, device=dev) if with_stats else None
+            _check(self._call(
+                self._fn_compress_batch, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
+                _ptr(status), _ptr(stats), ls.cuda_stream))
+            return EncodedBatch(out, oo, caps, sizes, status, stats)
 
     def decompress_batch(self, blobs, blob_offsets, blob_sizes, sample_counts, out=None, out_offsets=None,
                          stream: int | None = None):
         """Decode a device-resident batch; returns (samples int16 tensor, offsets, status)."""
         import torch
 
-        dev = blobs.device
-        n = int(sample_counts.numel())
-        counts = sample_counts.to(device=dev, dtype=torch.int32).contiguous()
-        if out_offsets is None:
-            so = torch.zeros(n, dtype=torch.int64, device=dev)
-            if n > 1:
-                so[1:] = torch.cumsum(counts.to(torch.int64), 0)[:-1]
-        else:
-            so = out_offsets.to(device=dev, dtype=torch.int64).contiguous()
-        if out is None:
-            total = int(counts.to(torch.int64).sum().item())
-            out = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
-        status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-        _check(self._call(
-            self._fn_decompress_batch, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
-            _ptr(blob_sizes.to(torch.int64).contiguous()), _ptr(out), _ptr(so), _ptr(counts), _ptr(status),
-            stream or 0))
-        return out, so, status
+        ls = self._launch_stream(stream)
+        with torch.cuda.stream(ls):
+            dev = blobs.device
+            n = int(sample_counts.numel())
+            counts = sample_counts.to(device=dev, dtype=torch.int32).contiguous()
+            if out_offsets is None:
+                so = torch.zeros(n, dtype=torch.int64, device=dev)
+                if n > 1:
+                    so[1:] = torch.cumsum(counts.to(torch.int64), 0)[:-1]
+            else:
+                so = out_offsets.to(device=dev, dtype=torch.int64).contiguous()
+            if out is None:
+                total = int(counts.to(torch.int64).sum().item())
+                out = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
+            status = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            _check(self._call(
+                self._fn_decompress_batch, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
+                _ptr(blob_sizes.to(torch.int64).contiguous()), _ptr(out), _ptr(so), _ptr(counts), _ptr(status),
+                ls.cuda_stream))
+            return out, so, status
 
     def synth_reads(self, nreads: int, samples_per_read, seed: int = 42, first_read: int = 0, read_stride: int = 1,
                     p_switch_q16: int = 6554, level_mean: int = 500, level_sd: int = 60, noise_sd: int = 12,
