@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--cpu-sample-reads", type=int, default=600)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-side", action="store_true",
+                   help="skip the STREAM-copy and PCIe-inclusive side measurements (profiling runs: the "
+                        "kernel statistics then hold only the bench batch's launches)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return p.parse_args()
 
@@ -154,7 +157,7 @@ def main():
     codec = PGNanoCodec(local)
     R, S = args.reads, args.samples
     side = {}
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not args.no_side:
         side["stream_copy_gbs"] = round(stream_copy_gbs(torch), 1)
         side["pcie_inclusive"] = pcie_inclusive(torch, codec, S, args.seed)
     # this rank's shard: global reads rank, rank + world, ... (round-robin)

@@ -6,4 +6,4 @@ shift || true
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-    python3 bench.py --no-cpu-baseline "$@" > gpurun_out/prof_$TAG.bench.log 2>&1
+    python3 bench.py --no-cpu-baseline --no-side "$@" > gpurun_out/prof_$TAG.bench.log 2>&1
