@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64) void dec_parse_kernel(DecArgs a)
     a.status[c] = c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], a.units + g * kStreams);
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void dec_zstd_kernel(DecArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void dec_zstd_kernel(DecArgs a)
 {
     const int lane = lane_id();
     const DecLayout lay = dec_layout();
