@@ -26,6 +26,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "MSamples/s encode+decode (1/2/4/8 GPU) at fixed ratio; % HBM roofline"
+# synthetic-read dwell per pore chemistry (R9.4.1 ~9, R10.4.1 ~12.5 samples per level):
+# p_switch in 1/65536 units
+PORES = {"default": 6554, "r941": 7282, "r103": 6554, "r1041": 5243}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
@@ -43,6 +46,14 @@ def parse():
                    help="skip the STREAM-copy and PCIe-inclusive side measurements (profiling runs: the "
                         "kernel statistics then hold only the bench batch's launches)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    # the other BASELINE configs; the default run is configs[1]
+    p.add_argument("--pore", choices=sorted(PORES), default="default",
+                   help="generator parameters: dwell per pore chemistry (configs[2] uses r1041)")
+    p.add_argument("--mixed-pores", action="store_true",
+                   help="configs[4]: thirds of the reads with R9.4.1 / R10.3 / R10.4.1 parameters")
+    p.add_argument("--decode-only", action="store_true", help="configs[4]: time the decode of the batch only")
+    p.add_argument("--compare-vbz", action="store_true",
+                   help="configs[2]: also encode the batch with VBZ (--VBZ) and report the size ratio")
     return p.parse_args()
 
 
@@ -165,7 +176,15 @@ def main():
     samples = torch.empty(R * S, dtype=torch.int16, device="cuda")
     counts = torch.full((R,), S, dtype=torch.int32, device="cuda")
     offs = torch.arange(R, dtype=torch.int64, device="cuda") * S
-    codec.synth_reads(R, S, seed=args.seed, first_read=sh.first_read, read_stride=sh.read_stride, out=samples)
+    if args.mixed_pores:  # thirds of the shard per chemistry
+        cuts = [0, R // 3, 2 * R // 3, R]
+        for i, pore in enumerate(("r941", "r103", "r1041")):
+            a, b = cuts[i], cuts[i + 1]
+            codec.synth_reads(b - a, S, seed=args.seed, first_read=sh.first_read + a * sh.read_stride,
+                              read_stride=sh.read_stride, p_switch_q16=PORES[pore], out=samples[a * S:b * S])
+    else:
+        codec.synth_reads(R, S, seed=args.seed, first_read=sh.first_read, read_stride=sh.read_stride,
+                          p_switch_q16=PORES[args.pore], out=samples)
     torch.cuda.synchronize()
     caps = torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
     boffs = torch.zeros(R, dtype=torch.int64, device="cuda")
@@ -179,6 +198,16 @@ def main():
         codec.decompress_batch(blobs, boffs, enc.sizes, counts, out=decoded, out_offsets=offs,
                                stream=codec.stream)
         return enc
+
+    if args.decode_only:  # configs[4]: the blobs are made once, outside the timed region
+        enc0 = codec.compress_batch(samples, offs, counts, out=blobs, out_offsets=boffs, out_caps=caps,
+                                    stream=codec.stream)
+        torch.cuda.synchronize()
+
+        def step():  # noqa: F811
+            codec.decompress_batch(blobs, boffs, enc0.sizes, counts, out=decoded, out_offsets=offs,
+                                   stream=codec.stream)
+            return enc0
 
     for _ in range(args.warmup):
         step()
@@ -212,21 +241,28 @@ def main():
         d_ms = sum(dec_ms) / len(dec_ms)
         # the hot path is a three-kernel pipeline per direction; the roofline is taken over the dominant
         # direction's launch sequence (HIP events on the codec stream around all its kernels)
-        dominant = "c5_decode" if d_ms >= e_ms else "c5_encode"
+        dominant = "c5_decode" if (d_ms >= e_ms or args.decode_only) else "c5_encode"
         kernels = codec.kernels(1 if dominant == "c5_decode" else 0)
-        k_ms = max(e_ms, d_ms)
+        k_ms = d_ms if args.decode_only else max(e_ms, d_ms)
         algo_bytes = (2.0 + comp_bytes / (R * S)) * R * S  # per launch on this GPU
         achieved = algo_bytes / (k_ms * 1e-3) / 1e9
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("reads") == R and tj.get("samples") == S:
+            if tj.get("reads") == R and tj.get("samples") == S and not (args.mixed_pores or args.pore != "default"):
                 traffic = tj.get(dominant)
         except (OSError, ValueError):
             pass
+        if args.mixed_pores:
+            gen = "configs[4]: mixed pores (thirds R9.4.1 / R10.3 / R10.4.1 generator dwell)"
+        elif args.pore != "default":
+            gen = f"configs[2]: {args.pore} generator dwell"
+        else:
+            gen = "configs[1]"
+        what = "C5 decode only" if args.decode_only else "C5 encode+decode"
         line = {
-            "metric": METRIC,
+            "metric": METRIC if not args.decode_only else "MSamples/s decode (configs[4]); % HBM roofline",
             "value": round(value, 2),
             "unit": "MSamples/s",
             "n_gpus": world,
@@ -239,7 +275,7 @@ def main():
             "dtype": "int16",
             "data": "synthetic (device generator: piecewise-constant levels + N(0,12) noise, integer-only)",
             "config": {
-                "workload": f"configs[1]: {R} reads x {S} int16 samples per GPU (1 chunk each), C5 encode+decode",
+                "workload": f"{gen}: {R} reads x {S} int16 samples per GPU (1 chunk each), {what}",
                 "reads_per_gpu": R,
                 "samples_per_read": S,
                 "parallelism": f"dp{world} (reads round-robin, no data-path collective)",
@@ -262,6 +298,17 @@ def main():
             },
         }
         line.update(side)
+        if args.compare_vbz and world == 1:  # the --VBZ side of the ratio comparison, outside the timing
+            from rawnanoporesignalcompression_amd import VBZCodec
+
+            vz = VBZCodec(local)
+            ev = vz.compress_batch(samples, offs, counts)
+            torch.cuda.synchronize()
+            vbytes = int(ev.sizes.sum().item())
+            line["vbz"] = {"bits_per_sample": round(8.0 * vbytes / (R * S), 4),
+                           "c5_vs_vbz_ratio": round(comp_bytes / max(vbytes, 1), 4),
+                           "status_ok": bool((ev.status == 0).all().item())}
+            vz.close()
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(S, args.cpu_sample_reads, args.seed) if world == 1 else None
             if line["cpu_baseline"]:

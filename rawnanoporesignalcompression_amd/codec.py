@@ -123,7 +123,9 @@ class PGNanoCodec:
     def _launch_stream(self, stream):
         """The HIP stream a batch call runs on (the caller's, else the context's), made to wait for
         the caller's current stream.  The call's own allocations and fills are issued on it too, so
-        they are ordered before the kernels and the caching allocator ties them to that stream."""
+        they are ordered before the kernels and the caching allocator ties them to that stream.  The
+        batch calls end by making the caller's current stream wait for it (an event, no host sync), so
+        the outputs are usable there like the results of any torch op."""
         import torch
 
         s = torch.cuda.ExternalStream(int(stream) if stream else self.stream, device=torch.device("cuda", self.device))
@@ -168,6 +170,7 @@ class PGNanoCodec:
         """
         import torch
 
+        caller = torch.cuda.current_stream()
         ls = self._launch_stream(stream)
         with torch.cuda.stream(ls):
             dev = samples.device
@@ -193,13 +196,15 @@ class PGNanoCodec:
             _check(self._call(
                 self._fn_compress_batch, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
                 _ptr(status), _ptr(stats), ls.cuda_stream))
-            return EncodedBatch(out, oo, caps, sizes, status, stats)
+        caller.wait_stream(ls)
+        return EncodedBatch(out, oo, caps, sizes, status, stats)
 
     def decompress_batch(self, blobs, blob_offsets, blob_sizes, sample_counts, out=None, out_offsets=None,
                          stream: int | None = None):
         """Decode a device-resident batch; returns (samples int16 tensor, offsets, status)."""
         import torch
 
+        caller = torch.cuda.current_stream()
         ls = self._launch_stream(stream)
         with torch.cuda.stream(ls):
             dev = blobs.device
@@ -219,7 +224,8 @@ class PGNanoCodec:
                 self._fn_decompress_batch, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
                 _ptr(blob_sizes.to(torch.int64).contiguous()), _ptr(out), _ptr(so), _ptr(counts), _ptr(status),
                 ls.cuda_stream))
-            return out, so, status
+        caller.wait_stream(ls)
+        return out, so, status
 
     def synth_reads(self, nreads: int, samples_per_read, seed: int = 42, first_read: int = 0, read_stride: int = 1,
                     p_switch_q16: int = 6554, level_mean: int = 500, level_sd: int = 60, noise_sd: int = 12,
