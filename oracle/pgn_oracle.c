@@ -14,6 +14,11 @@
  * htslib, and pod5_format_export.h is CMake-generated), so this restatement is the oracle.  See
  * DESIGN.md "Oracle and parity" for how it is pinned.
  *
+ * The other compile-time variants (C4, C1, C2, C3, VBZ0; pgno_variant_*) have no reference fixture,
+ * test or runnable build: their restatement is PARITY UNPINNED by reference output -- it is checked
+ * only by hand-computed layouts and by its relations to the pinned VBZ/C5 restatements
+ * (tests/test_oracle_variants.py).
+ *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
  */
 #include <dlfcn.h>
