@@ -1240,14 +1240,23 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     }
     wave_sync();
     {
-        uint32_t rank[4] = {0, 0, 0, 0};
-        for (uint32_t t = 0; t <= maxSym; t++) {
-            uint32_t ct = L.count[t];
+        // one compare per pair on the key count << 8 | (255 - symbol): t ranks before s iff
+        // count_t > count_s, or equal counts and t < s; four counts per round of loads
+        uint32_t rank[4] = {0, 0, 0, 0}, key[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                uint32_t s = (uint32_t)lane + 64u * (uint32_t)q;
-                rank[q] += (ct > c[q]) || (ct == c[q] && t < s);
+        for (int q = 0; q < 4; q++) key[q] = (c[q] << 8) | (255u - ((uint32_t)lane + 64u * (uint32_t)q));
+        const uint32_t T = maxSym + 1;
+        for (uint32_t t0 = 0; t0 < T; t0 += 4) {
+            uint32_t kt[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t t = t0 + (uint32_t)u;
+                kt[u] = (t < T) ? ((L.count[t] << 8) | (255u - t)) : 0u;
             }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) rank[q] += kt[u] > key[q] ? 1u : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
