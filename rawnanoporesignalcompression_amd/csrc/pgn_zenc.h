@@ -1199,11 +1199,18 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
             const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
             const uint32_t sa = i / segSize;
             const uint32_t boundary = (sa + 1) * segSize;
+            if (i + 16 <= n && i + 16 <= boundary) {  // the usual case: 16 bytes of one segment
+                uint32_t* h = &L.hist2[sa >> 1][0];
+                const uint32_t inc = 1u << (16 * (sa & 1));
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if (i + k < n) {
-                    const uint32_t sg = (i + k < boundary) ? sa : sa + 1;
-                    atomicAdd(&L.hist2[sg >> 1][(wd[k >> 2] >> (8 * (k & 3))) & 0xFFu], 1u << (16 * (sg & 1)));
+                for (int k = 0; k < 16; k++) atomicAdd(h + ((wd[k >> 2] >> (8 * (k & 3))) & 0xFFu), inc);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    if (i + k < n) {
+                        const uint32_t sg = (i + k < boundary) ? sa : sa + 1;
+                        atomicAdd(&L.hist2[sg >> 1][(wd[k >> 2] >> (8 * (k & 3))) & 0xFFu], 1u << (16 * (sg & 1)));
+                    }
                 }
             }
         }
