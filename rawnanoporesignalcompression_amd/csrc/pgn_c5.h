@@ -132,12 +132,16 @@ __device__ __forceinline__ uint32_t split_step(const uint4& a, const uint4& b, c
     const uint32_t t12 = readlane_u32(i12, 63), t3 = readlane_u32(i3, 63);
     const uint32_t e12 = i12 - p12;
     uint32_t qS = fS + (e12 & 0xFFFFu), qM = fM + (e12 >> 16), qL = fL + (i3 - n3);
-    const uint32_t dS = kDummy + 4u * lane;
+    // one LDS byte per sample: the S or M window slot of its class (classes 0 and 3: a per-lane
+    // discard slot in the S window)
+    uint8_t* const wb = reinterpret_cast<uint8_t*>(&W);
+    constexpr uint32_t offS = (uint32_t)__builtin_offsetof(SplitLds, S), offM = (uint32_t)__builtin_offsetof(SplitLds, M);
+    const uint32_t dS = offS + kDummy + 4u * lane;
 #pragma unroll
     for (int m = 0; m < 16; m++) {
         const uint32_t c = (kw >> (2 * m)) & 3u;
-        W.S[c == 1 ? qS : dS] = (uint8_t)(v[m] - ClassOffsets<C4>::o1);
-        W.M[c == 2 ? qM : dS] = (uint8_t)(v[m] - ClassOffsets<C4>::o2);
+        const uint32_t at = (c == 1) ? offS + qS : ((c == 2) ? offM + qM : dS);
+        wb[at] = (uint8_t)(v[m] - ((c == 1) ? ClassOffsets<C4>::o1 : ClassOffsets<C4>::o2));
         qS += (c == 1);
         qM += (c == 2);
     }
