@@ -105,7 +105,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     // staged bytes of the round: loaded one round ahead from the estimate of the next round's
     // position (T drops by 16W, minus at most tl - 1 bits; round_base leaves room for both)
     int32_t base = round_base(T - j * kWinBits);
-    uint4 nx[3];
+    uint4 nx[kStgWords / 4];
     round_load(nx, src, sl, base);
 #ifdef PGN_DEBUG_HUF
     hdbg(1, (uint32_t)k, (uint32_t)j, (uint32_t)T, (uint32_t)sl, nsym, tl, rs);
@@ -115,7 +115,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         const int32_t lo = (hi - kWinBits > 0) ? hi - kWinBits : 0;
         const int32_t b8 = 8 * base;
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
+        for (int i = 0; i < kStgWords / 4; i++) {
             sDec.stg[4 * i][lane] = nx[i].x;
             sDec.stg[4 * i + 1][lane] = nx[i].y;
             sDec.stg[4 * i + 2][lane] = nx[i].z;

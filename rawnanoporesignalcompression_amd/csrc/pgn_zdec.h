@@ -9,9 +9,9 @@
 
 namespace pgn {
 
-constexpr int32_t kWinBits = 256;        // Huffman stream bits per lane per round (pgn_huf4.h)
+constexpr int32_t kWinBits = 384;        // Huffman stream bits per lane per round (pgn_huf4.h)
 constexpr int kBmpBits = 128;            // speculative boundaries recorded per lane: bit d = position hi - d
-constexpr int kStgWords = 12;            // staged bytes per lane per round: 48 >= (256 + 63) / 8 + 8
+constexpr int kStgWords = 16;            // staged bytes per lane per round: 64 >= (384 + 63) / 8 + 8
 
 constexpr int kSeqWin = 2048;            // sequences bitstream window staged in LDS
 constexpr int kSeqHdr = 400;             // staged sequences-section header (table descriptions)
@@ -116,14 +116,14 @@ __device__ __forceinline__ uint32_t ld_word(const uint8_t* s, int32_t sl, int32_
 // estimate it was staged for; it stages bytes [base, base + 48) with base = 4 * floor((est - W -
 // 32) / 32), so bits [q - tl, q) of every q in the window and the 64-bit reads above them are inside.
 __device__ __forceinline__ int32_t round_base(int32_t hi) { return ((hi - kWinBits - 32) >> 5) * 4; }
-__device__ __forceinline__ void round_load(uint4 v[3], const uint8_t* s, int32_t sl, int32_t base)
+__device__ __forceinline__ void round_load(uint4 v[kStgWords / 4], const uint8_t* s, int32_t sl, int32_t base)
 {
     if (base >= 0 && base + 4 * kStgWords <= sl) {
 #pragma unroll
-        for (int i = 0; i < 3; i++) v[i] = gld<uint4>(s + base + 16 * i);
+        for (int i = 0; i < kStgWords / 4; i++) v[i] = gld<uint4>(s + base + 16 * i);
     } else {
 #pragma unroll
-        for (int i = 0; i < 3; i++)
+        for (int i = 0; i < kStgWords / 4; i++)
             v[i] = make_uint4(ld_word(s, sl, base + 16 * i), ld_word(s, sl, base + 16 * i + 4),
                               ld_word(s, sl, base + 16 * i + 8), ld_word(s, sl, base + 16 * i + 12));
     }
