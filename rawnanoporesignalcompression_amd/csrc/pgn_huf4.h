@@ -129,11 +129,20 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         }
         lds_sync();
         // ---- pass A: speculative decode of (lo, hi]: symbol count c, exit q
-        int32_t q = hi;
+        // lanes 1..15 start kOvBits above their window (inside the staged bytes: 8 * base + 32 *
+        // kStgWords >= hi + 65), so the speculative path has usually merged with the true one by hi
+        // and the sync below finds the true entry among the recorded boundaries without a walk
+        int32_t q = (j == 0 || hi <= lo) ? hi : hi + kOvBits;
         uint32_t c = 0;
         {
             StgBits r;
             stg_init(r, lane, q - b8 - tli);
+            while (ballot(q > hi)) {  // overlap: decoded, neither counted nor recorded
+                uint32_t e[2];
+                stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
+#pragma unroll
+                for (int u = 0; u < 2; u++) q = q > hi ? q - (int32_t)(e[u] >> 8) : q;
+            }
             while (ballot(q > lo && hi - q < kBmpBits)) {
                 uint32_t e[2];
                 stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
@@ -187,18 +196,20 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             if (need) {
                 int32_t p = entry;
                 uint32_t w = 0;
-                bool synced = false;
-                StgBits r;
-                stg_init(r, lane, p - b8 - tli);
-                while (p > lo) {
-                    const int32_t d = hi - p;
-                    if (d < kBmpBits && (((d < 64 ? (bm0 >> d) : (bm1 >> (d - 64))) & 1ull) != 0)) {
-                        synced = true;
-                        break;
-                    }
-                    const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
-                    p -= (int32_t)(e >> 8);
-                    w++;
+                // a recorded boundary at p (none lies at or below lo: kBmpBits < kWinBits)
+                auto recorded = [&](int32_t pp) {
+                    const int32_t d = hi - pp;
+                    return d < kBmpBits && (((d < 64 ? (bm0 >> d) : (bm1 >> (d - 64))) & 1ull) != 0);
+                };
+                bool synced = recorded(p);
+                if (!synced && p > lo) {  // walk the true path until it meets a recorded boundary
+                    StgBits r;
+                    stg_init(r, lane, p - b8 - tli);
+                    do {
+                        const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
+                        p -= (int32_t)(e >> 8);
+                        w++;
+                    } while (p > lo && !(synced = recorded(p)));
                 }
                 if (synced) {
                     const int32_t d = hi - p;

@@ -10,6 +10,7 @@
 namespace pgn {
 
 constexpr int32_t kWinBits = 384;        // Huffman stream bits per lane per round (pgn_huf4.h)
+constexpr int32_t kOvBits = 64;         // speculative overlap above a lane's window (pgn_huf4.h)
 constexpr int kBmpBits = 128;            // speculative boundaries recorded per lane: bit d = position hi - d
 constexpr int kStgWords = 16;            // staged bytes per lane per round: 64 >= (384 + 63) / 8 + 8
 
