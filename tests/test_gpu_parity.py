@@ -196,3 +196,46 @@ def test_decode_frames_from_other_encoder_settings(codec):
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
     assert np.array_equal(out.cpu().numpy()[: counts.sum()], np.concatenate(want))
+
+
+def _huffman_stress_signals():
+    """Delta distributions from very skewed (1-2 bit Huffman codes, hundreds of symbols per lane
+    window) to wide (11-bit codes): every shape the speculative Huffman rounds must resynchronise on."""
+    rng = np.random.default_rng(11)
+    sig = {}
+    for p in (0.97, 0.9, 0.6, 0.3, 0.1, 0.03):
+        d = rng.geometric(p, 131072) - 1
+        d = np.where(rng.random(d.size) < 0.5, d, -d)
+        sig[f"geometric_p{p}"] = np.cumsum(d).astype(np.int16)
+    for sd in (1, 40, 3000):
+        sig[f"gauss_sd{sd}"] = (np.cumsum(rng.normal(0, sd, 102400)).round() % 65536 - 32768).astype(np.int16)
+    sig["mostly_zero_deltas"] = np.cumsum((rng.random(102400) < 0.002) * rng.integers(-9, 10, 102400)).astype(np.int16)
+    return sig
+
+
+@pytest.mark.gpu
+def test_huffman_stress_signals_identical(codec):
+    """Encoder bytes = oracle bytes, and the GPU decoder round-trips the oracle's blob, one at a time
+    and batched (the batched path runs the staged decode kernels)."""
+    import torch
+
+    sigs = list(_huffman_stress_signals().items())
+    blobs = []
+    for name, x in sigs:
+        rc, ref, _ = O.c5_compress(x)
+        if rc != 0:  # wider than max(2n+26, 1024): the reference refuses it as well
+            continue
+        assert codec.compress_signal(x) == ref, name
+        assert np.array_equal(codec.decompress_signal(ref, sample_count=x.size), x), name
+        blobs.append((ref, x))
+    assert len(blobs) >= 8
+    sizes = np.array([len(b) for b, _ in blobs], np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    flat = np.frombuffer(b"".join(b for b, _ in blobs), np.uint8)
+    counts = np.array([x.size for _, x in blobs], np.int32)
+    dev = torch.device("cuda", 0)
+    out, so, st = codec.decompress_batch(torch.from_numpy(flat.copy()).to(dev), torch.from_numpy(offs).to(dev),
+                                         torch.from_numpy(sizes).to(dev), torch.from_numpy(counts).to(dev))
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert np.array_equal(out.cpu().numpy()[: counts.sum()], np.concatenate([x for _, x in blobs]))
