@@ -28,25 +28,41 @@ struct alignas(16) DecLds {
     union {
         struct {  // literals stage
             uint16_t tab[1u << kHufLdsLog];   // Huffman decode table: symbol | nbBits << 8
-            // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
-            uint32_t stg[kStgWords][64];      // staged stream bytes of the current round
-            uint8_t wts[256];                 // weights of the current table
-            uint8_t order[256];               // symbols sorted by (weight, symbol)
-            uint8_t hbuf[272];                // staged Huffman table description (zero padded)
-            z1::FseDEntry wdt[64];            // weights FSE decode table (tableLog <= 6)
-            int16_t wnorm[16];
-            uint16_t wnext[16];
-            uint32_t wrank[16];
+            union {
+                // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
+                uint32_t stg[kStgWords][64];  // staged stream bytes of the current round
+                struct {                      // table build only (done before the rounds start)
+                    uint8_t wts[256];         // weights of the current table
+                    uint8_t order[256];       // symbols sorted by (weight, symbol)
+                    uint8_t hbuf[272];        // staged Huffman table description (zero padded)
+                    z1::FseDEntry wdt[64];    // weights FSE decode table (tableLog <= 6)
+                    int16_t wnorm[16];
+                    uint16_t wnext[16];
+                    uint32_t wrank[16];
+                };
+            };
         };
         struct {  // sequences stage
             uint32_t qtab[kSeqTab];           // FSE entries: newState | symbol << 16 | nbBits << 24
-            int16_t qnorm[64];
             uint32_t qsq[64][3];              // a batch of decoded sequences: litLength, matchLength, offset
-            uint8_t qhdr[kSeqHdr];
-            uint8_t qwin[kSeqWin];
+            union {
+                struct {                      // section head and table build (before the bitstream)
+                    int16_t qnorm[64];
+                    uint8_t qhdr[kSeqHdr];
+                };
+                uint8_t qwin[kSeqWin];        // bitstream window
+            };
         };
     };
-    uint32_t u[16];
+};
+// 8 KiB: 20 one-wave workgroups per CU (160 KiB of LDS)
+static_assert(sizeof(DecLds) <= 8192, "decoder LDS exceeds 8 KiB");
+
+// Frame state of the sequences stage, carried across the blocks of a frame.
+struct SeqState {
+    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;  // repeat offsets
+    uint32_t valid = 0;                      // bit k: table k valid (repeat mode)
+    uint32_t saved = 0;                      // bit k: table k saved to S.tables (multi-block frames)
 };
 
 // One instance per decode workgroup (namespace scope, so every access is a DS instruction).
@@ -484,8 +500,7 @@ __device__ __noinline__ bool huf_decode1_lane(unsigned tl, const uint8_t* src, s
 // Sequences (ZSTD_decodeSeqHeaders + ZSTD_decodeSequence + execution), wave-uniform.  The three FSE
 // decode tables are built in LDS (the predefined ones are copied from gSeqDefTab); the bitstream
 // is read backwards through a window staged into LDS; sequences are decoded 64 at a time into LDS
-// and executed by the whole wave.  Frame state lives in sDec.u: [2..4] repeat offsets, [5] bit k =
-// table k valid (repeat mode), [6] bit k = table k saved to S.tables (multi-block frames).
+// and executed by the whole wave.  Frame state (SeqState) is the caller's, passed by reference.
 // ---------------------------------------------------------------------------------------------
 __device__ uint32_t gSeqDefTab[kSeqTab + 4];  // predefined LL / OF / ML tables (+ their logs), filled once
 
@@ -601,7 +616,7 @@ __device__ __forceinline__ uint32_t seqbits_read(SeqBits& b, uint32_t nb)
 // One block's sequences: decode + execute.  Returns the new output position or a negative DecErr.
 __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t seqSize, const uint8_t* lit, size_t rs,
                                                  uint8_t* dst, size_t op, size_t dstCap, size_t frameStart,
-                                                 DecScratch S, bool lastBlock)
+                                                 DecScratch S, bool lastBlock, SeqState& fs)
 {
     const int lane = lane_id();
     seqSrc = uni(seqSrc);
@@ -633,8 +648,9 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
             pos = 2;
         }
     }
-    uint32_t rep0 = sDec.u[2], rep1 = sDec.u[3], rep2 = sDec.u[4];
-    uint32_t valid = sDec.u[5];
+    uint32_t rep0 = uni(fs.rep0), rep1 = uni(fs.rep1), rep2 = uni(fs.rep2);
+    uint32_t valid = uni(fs.valid);
+    const uint32_t saved = uni(fs.saved);
     if (nbSeq == 0) {
         if (pos != srcSize) return z1::kDecErrCorrupt;
     } else {
@@ -668,7 +684,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
                 tlog[k] = tl;
                 pos += (int32_t)nc;
             } else {  // repeat: the previous block's table (saved to HBM)
-                if (!((valid >> k) & 1u) || !((sDec.u[6] >> k) & 1u)) return z1::kDecErrCorrupt;
+                if (!((valid >> k) & 1u) || !((saved >> k) & 1u)) return z1::kDecErrCorrupt;
                 const uint32_t lg = S.tables[kSeqTab + k];
                 for (uint32_t u = (uint32_t)lane; u < (1u << lg); u += 64) sDec.qtab[off + u] = S.tables[off + u];
                 tlog[k] = lg;
@@ -682,7 +698,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
                 for (uint32_t u = (uint32_t)lane; u < (1u << tlog[k]); u += 64) gst<uint32_t>(S.tables + off + u, sDec.qtab[off + u]);
                 if (lane == 0) gst<uint32_t>(S.tables + kSeqTab + k, tlog[k]);
             }
-            if (lane == 0) sDec.u[6] = 7u;
+            fs.saved = 7u;
         }
         // bitstream
         SeqBits br;
@@ -770,13 +786,10 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
         wave_copy(dst + op, lit + litPos, remLit);
         op += remLit;
         lds_sync();
-        if (lane == 0) {
-            sDec.u[2] = rep0;
-            sDec.u[3] = rep1;
-            sDec.u[4] = rep2;
-            sDec.u[5] = valid;
-        }
-        lds_sync();
+        fs.rep0 = rep0;
+        fs.rep1 = rep1;
+        fs.rep2 = rep2;
+        fs.valid = valid;
         return (long)op;
     }
     // no sequences: the literals are the block
@@ -839,14 +852,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
         bool hufInLds = false;  // ... and is in sDec.tab (tables up to kHufLdsLog)
         bool hufParked = false; // ... and a copy is parked in S.htab
         unsigned hufTl = 0;
-        if (lane == 0) {  // frame state of the sequences stage: repeat offsets, table validity
-            sDec.u[2] = 1;
-            sDec.u[3] = 4;
-            sDec.u[4] = 8;
-            sDec.u[5] = 0;
-            sDec.u[6] = 0;
-        }
-        lds_sync();
+        SeqState fs;  // frame state of the sequences stage: repeat offsets, table validity
         while (true) {
             if (srcSize - ip < 3) return z1::kDecErrSrcSmall;
             const uint32_t bh = (uint32_t)gb(src + (ip)) | ((uint32_t)gb(src + (ip + 1)) << 8) | ((uint32_t)gb(src + (ip + 2)) << 16);
@@ -949,7 +955,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     }
                     hufInLds = false;
                     wave_sync();
-                    const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, last != 0);
+                    const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, last != 0, fs);
                     if (r < 0) return r;
                     op = (size_t)r;
                     P.mark(4);
