@@ -10,14 +10,15 @@
  * install_dependencies.sh:10; pod5/c++/CMakeLists.txt:18 find_package(zstd)).  This image ships
  * libzstd 1.4.9 (/opt/conda/lib) and 1.4.8 (system); it is dlopen()ed here, 1.4.9 first.
  *
- * The compiled reference is NOT buildable in this image (C5.hpp pulls BAM_handler.h -> boost +
- * htslib, and pod5_format_export.h is CMake-generated), so this restatement is the oracle.  See
- * DESIGN.md "Oracle and parity" for how it is pinned.
- *
- * The other compile-time variants (C4, C1, C2, C3, VBZ0; pgno_variant_*) have no reference fixture,
- * test or runnable build: their restatement is PARITY UNPINNED by reference output -- it is checked
- * only by hand-computed layouts and by its relations to the pinned VBZ/C5 restatements
- * (tests/test_oracle_variants.py).
+ * The whole reference codec is not buildable in this image (the pgnano:: compress/decompress bodies
+ * pull BAM_handler.h -> boost + htslib, and pod5_format_export.h is CMake-generated).  Its svb16
+ * split/merge stage IS: oracle/ref.mk compiles the `namespace svb16` block of every variant header
+ * (C5, C4, C3, C2, C1, VBZ_0) and the pod5 VBZ svb16 stage verbatim from /root/reference into
+ * oracle/_ref/, and tests/test_oracle_ref.py holds this restatement's split streams, merge outputs and
+ * consumed counts (pgno_variant_streams / pgno_variant_merge / pgno_vbz_svb_encode) to it on the
+ * reference fixture, edge sizes, stress and fuzz inputs.  The frame assembly around it (u64 length
+ * prefixes, ZSTD_compress level 1, content-size bookkeeping) is pinned by the reference's own VBZ
+ * fixture blobs and by reading C5.hpp:282-683 line by line.  See DESIGN.md "Oracle and parity".
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library.
  */
@@ -835,6 +836,23 @@ int pgno_variant_decompress(int variant, const uint8_t *src, size_t len, int16_t
     }
     if (rc != PGNO_OK) return rc;
     return consumed == total ? PGNO_OK : PGNO_ERR_REMAINING;
+}
+
+/* The merge stage alone over a caller-built intermediate (tests/test_oracle_ref.py holds it to the
+ * reference's compiled decode_* on the same bytes).  d[s] = decompressed size of frame s, as the
+ * reference passes them; *consumed = the count the reference compares with the intermediate size. */
+int pgno_variant_merge(int variant, const uint8_t *inter, uint64_t total, const uint64_t d[5], int16_t *out,
+                       uint32_t n, uint64_t *consumed)
+{
+    switch (variant) {
+    case PGNO_V_C5: return c5_merge(inter, total, d[1], d[2], d[3], out, n, consumed);
+    case PGNO_V_C4: return c4_merge(inter, total, d[1], d[2], d[3], out, n, consumed);
+    case PGNO_V_C1: return c1_merge(inter, total, out, n, consumed);
+    case PGNO_V_C2: return c23_merge(inter, total, d[1], 0, out, n, consumed, 0);
+    case PGNO_V_C3: return c23_merge(inter, total, d[1], d[2], out, n, consumed, 1);
+    case PGNO_V_VBZ0: return vbz0_merge(inter, total, out, n, consumed);
+    }
+    return PGNO_ERR_ALLOC;
 }
 
 /* raw streams of a variant (tests: GPU split checks, blobs from other encoder settings) */

@@ -50,6 +50,8 @@ def oracle() -> C.CDLL:
                                             C.POINTER(C.c_size_t), C.c_void_p]
         L.pgno_variant_decompress.argtypes = [C.c_int, C.c_void_p, C.c_size_t, C.c_void_p, C.c_uint32]
         L.pgno_variant_streams.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        L.pgno_variant_merge.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p]
         L.pgno_vbz0_encode.restype = C.c_size_t
         L.pgno_vbz0_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         L.pgno_synth_read.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint32, C.c_int32,
@@ -220,3 +222,113 @@ def variant_assemble(frames: list[bytes]) -> bytes:
             out += len(f).to_bytes(8, "little")
         out += f
     return out
+
+
+def oracle_variant_merge(variant: str, inter: bytes, d: list[int], n: int):
+    """The restatement's merge over an intermediate: (status, samples, consumed count)."""
+    L = oracle()
+    a = _buf(inter)
+    dd = np.zeros(5, np.uint64)
+    dd[: len(d)] = d
+    out = np.zeros(max(n, 1), np.int16)
+    consumed = C.c_uint64(0)
+    rc = L.pgno_variant_merge(VARIANTS[variant], a.ctypes.data, len(inter), dd.ctypes.data, out.ctypes.data, n,
+                              C.byref(consumed))
+    return rc, out[:n], int(consumed.value)
+
+
+def oracle_vbz_svb_encode(x: np.ndarray) -> bytes:
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    out = np.zeros(3 * x.size + 16, np.uint8)
+    m = oracle().pgno_vbz_svb_encode(x.ctypes.data if x.size else 0, x.size, out.ctypes.data)
+    return out[:m].tobytes()
+
+
+# ------------------------------------------------------------------------------------------------
+# The reference's own svb16 stages, compiled verbatim from /root/reference by oracle/ref.mk into
+# oracle/_ref/ (absent on the GPU box and wherever /root/reference is not mounted: ref() is then None).
+# ------------------------------------------------------------------------------------------------
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libpgn_ref.so")
+REF_VBZ_SO = os.path.join(ROOT, "oracle", "_ref", "libpgn_ref_vbz.so")
+REF_SRC = "/root/reference/pod5/c++/pod5_format/pgnano/svb16/C5.hpp"
+_r = None
+_rv = None
+
+
+def ref():
+    """libpgn_ref.so (the reference's svb16 split/merge of every variant), built when the reference tree
+    is present; None when neither the library nor the reference sources exist."""
+    global _r, _rv
+    if _r is None:
+        if not (os.path.exists(REF_SO) and os.path.exists(REF_VBZ_SO)):
+            if not os.path.exists(REF_SRC):
+                return None
+            subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-f", "ref.mk"], check=True,
+                           capture_output=True)
+        L = C.CDLL(REF_SO)
+        L.pgnr_encode.restype = C.c_int
+        L.pgnr_encode.argtypes = [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.pgnr_decode.restype = C.c_int64
+        L.pgnr_decode.argtypes = [C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32]
+        L.pgnr_counters.argtypes = [C.c_void_p, C.c_int]
+        V = C.CDLL(REF_VBZ_SO)
+        V.pgnr_vbz_svb_encode.restype = C.c_size_t
+        V.pgnr_vbz_svb_encode.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        V.pgnr_vbz_svb_decode.restype = C.c_size_t
+        V.pgnr_vbz_svb_decode.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32]
+        V.pgnr_vbz_padding.restype = C.c_size_t
+        _r, _rv = L, V
+    return _r
+
+
+def ref_vbz():
+    return _rv if ref() is not None else None
+
+
+def ref_variant_streams(variant: str, x: np.ndarray) -> list[bytes]:
+    """The streams the reference's own svb16 encode_* hands to ZSTD_compress, one per frame."""
+    L = ref()
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    n = x.size
+    buf = np.zeros(5 * (n + 64) + 3 * n + 64, np.uint8)
+    offs = np.zeros(5, np.uint64)
+    sz = np.zeros(5, np.uint64)
+    nf = L.pgnr_encode(VARIANTS[variant], x.ctypes.data if n else 0, n, buf.ctypes.data, offs.ctypes.data,
+                       sz.ctypes.data)
+    assert nf > 0
+    return [buf[int(offs[s]): int(offs[s]) + int(sz[s])].tobytes() for s in range(nf)]
+
+
+def ref_counters(reset: bool = True) -> dict:
+    """number_small / number_medium / number_large as the reference's encode_scalar_N01 counts them."""
+    out = np.zeros(10, np.int64)
+    ref().pgnr_counters(out.ctypes.data, 1 if reset else 0)
+    return {"small": int(out[0]), "medium": int(out[1]), "large": int(out[2])}
+
+
+def ref_variant_merge(variant: str, inter: bytes, d: list[int], n: int):
+    """The reference's decode_* over an intermediate: (samples, consumed count)."""
+    a = _buf(inter)
+    dd = np.zeros(5, np.uint64)
+    dd[: len(d)] = d
+    out = np.zeros(max(n, 1), np.int16)
+    consumed = ref().pgnr_decode(VARIANTS[variant], a.ctypes.data, len(inter), dd.ctypes.data, out.ctypes.data, n)
+    return out[:n], int(consumed)
+
+
+def ref_vbz_svb_encode(x: np.ndarray) -> bytes:
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    out = np.zeros(3 * x.size + 16, np.uint8)
+    m = ref_vbz().pgnr_vbz_svb_encode(x.ctypes.data if x.size else 0, x.size, out.ctypes.data)
+    return out[:m].tobytes()
+
+
+def ref_vbz_svb_decode(inter: bytes, n: int):
+    """(samples, consumed) from the reference's svb16::decode; the buffer carries its padding bytes."""
+    V = ref_vbz()
+    pad = int(V.pgnr_vbz_padding())
+    a = np.zeros(len(inter) + pad + 16, np.uint8)
+    a[: len(inter)] = np.frombuffer(inter, np.uint8)
+    out = np.zeros(max(n, 1), np.int16)
+    consumed = V.pgnr_vbz_svb_decode(a.ctypes.data, len(inter) + pad, out.ctypes.data, n)
+    return out[:n], int(consumed)

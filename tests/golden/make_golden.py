@@ -6,7 +6,10 @@ Inputs are data only:
     pod5/test_data/multi_fast5_zip_v3.pod5 (VBZ-compressed real nanopore signal, 22 chunks), read with
     pyarrow from the file's embedded Arrow IPC signal table;
   * synthetic reads from the checker's generator.
-Expected outputs come from the oracle (oracle/pgn_oracle.c over libzstd 1.4.9).
+Expected outputs come from the oracle (oracle/pgn_oracle.c over libzstd 1.4.9).  The C5 split of every
+fixture chunk is also produced by the reference's OWN svb16 code (oracle/_ref/libpgn_ref.so, compiled
+verbatim from C5.hpp:27-277 by oracle/ref.mk): those digests are recorded as `ref_streams_sha256`
+(after asserting the oracle's streams equal them) so the pin travels without the reference tree.
 
 Usage: python tests/golden/make_golden.py [/path/to/multi_fast5_zip_v3.pod5]
 """
@@ -50,6 +53,7 @@ def read_signal_table(path: str):
 
 
 def main(path: str = POD5) -> None:
+    assert O.ref() is not None, "the reference check needs /root/reference (oracle/ref.mk)"
     blobs, counts, read_ids = read_signal_table(path)
     offs = np.cumsum([0] + [len(b) for b in blobs]).astype(np.int64)
     np.savez_compressed(os.path.join(HERE, "pod5_v3_signal.npz"),
@@ -65,7 +69,9 @@ def main(path: str = POD5) -> None:
         assert rc == 0
         rc2, back = O.c5_decompress(c5, n)
         assert rc2 == 0 and np.array_equal(back, x)
-        real.append({"chunk": i, "read_id": read_ids[i], "samples": n, "signal_sha256": sha(x.tobytes()),
+        ref_streams = O.ref_variant_streams("C5", x)
+        assert ref_streams == O.variant_streams("C5", x), f"chunk {i}: oracle split differs from the reference"
+        real.append({"ref_streams_sha256": [sha(b) for b in ref_streams], "chunk": i, "read_id": read_ids[i], "samples": n, "signal_sha256": sha(x.tobytes()),
                      "vbz_size": len(b), "vbz_reencode_identical": vbz_again == b,
                      "c5_size": len(c5), "c5_sha256": sha(c5), "streams": [int(v) for v in st]})
         tot_c5 += len(c5)
@@ -94,6 +100,8 @@ def main(path: str = POD5) -> None:
     doc = {
         "generator": "tests/golden/make_golden.py",
         "zstd_version": int(O.oracle().pgno_zstd_version()),
+        "ref_pinned": {"c5_streams": True, "library": "oracle/_ref/libpgn_ref.so",
+                       "recipe": "oracle/ref.mk (C5.hpp:27-277 compiled verbatim)"},
         "real": real,
         "real_totals": {"samples": tot_n, "c5_bits_per_sample": 8.0 * tot_c5 / tot_n,
                         "vbz_bits_per_sample": 8.0 * tot_vbz / tot_n},
