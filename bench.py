@@ -7,19 +7,32 @@ integer-only generator the checker uses.  One step = encode every chunk + decode
 inputs already resident in HBM.  value = samples / (t_enc + t_dec) over all ranks (weak scaling:
 each rank owns its own 100k-read shard; reads are assigned round-robin, read r -> rank r % N).
 
+configs[3] (--global-reads 1000000): a fixed global read set split round-robin over the ranks
+(strong scaling), each rank working through its share in resident batches of at most --reads reads.
+
+Multi-GPU: one process per GPU.  Under torchrun the rank comes from the environment; `--gpus N`
+without a torchrun environment starts N worker processes itself (before anything touches the GPU)
+with the same environment torchrun would give them.  The only exchange is the final size/ratio
+reduction (RCCL all-reduce over xGMI) and the max-over-ranks time.
+
 The dominant kernel's roofline is measured live with HIP events on the launch stream; the CPU
 baseline is the oracle (the libzstd-backed C restatement of the reference's C5 path) on one host
-thread over a bounded sample.
+thread over a bounded sample, plus an all-cores leg (reads sharded over the box's CPU share).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--samples S]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--reads R] [--samples S] [--global-reads G]
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
+import glob
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -32,20 +45,25 @@ PORES = {"default": 6554, "r941": 7282, "r103": 6554, "r1041": 5243}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--reads", type=int, default=100_000, help="reads per GPU")
+    p.add_argument("--reads", type=int, default=100_000, help="reads per GPU (per resident batch with --global-reads)")
     p.add_argument("--samples", type=int, default=100_000, help="samples per read")
+    p.add_argument("--global-reads", type=int, default=0,
+                   help="configs[3]: a fixed global read count split round-robin over the ranks (strong scaling)")
     p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                   help="nccl (= RCCL) for one process per GPU; gloo lets several ranks share one GPU (rehearsal)")
     p.add_argument("--cpu-sample-reads", type=int, default=600)
+    p.add_argument("--cpu-threads", type=int, default=0, help="all-cores CPU leg threads (0 = the box's CPU share)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-side", action="store_true",
-                   help="skip the STREAM-copy and PCIe-inclusive side measurements (profiling runs: the "
-                        "kernel statistics then hold only the bench batch's launches)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+                   help="skip the STREAM-copy, PCIe-inclusive and per-chunk side measurements (profiling runs: "
+                        "the kernel statistics then hold only the bench batch's launches)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     # the other BASELINE configs; the default run is configs[1]
     p.add_argument("--pore", choices=sorted(PORES), default="default",
                    help="generator parameters: dwell per pore chemistry (configs[2] uses r1041)")
@@ -54,15 +72,78 @@ def parse():
     p.add_argument("--decode-only", action="store_true", help="configs[4]: time the decode of the batch only")
     p.add_argument("--compare-vbz", action="store_true",
                    help="configs[2]: also encode the batch with VBZ (--VBZ) and report the size ratio")
-    return p.parse_args()
+    return p.parse_args(argv)
+
+
+# ---- multi-process launch (no GPU in the parent) ------------------------------------------------
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_workers(n: int, argv: list[str], script: str | None = None, timeout: float | None = None) -> int:
+    """Start n worker processes of `script` (default: this file) with torchrun's environment (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for them.  The parent never
+    touches the GPU; if a worker fails the others are terminated.  Returns the first non-zero exit
+    status (0 when all succeed)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    t0 = time.monotonic()
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code
+                for o in live:
+                    procs[o].terminate()
+        if timeout is not None and time.monotonic() - t0 > timeout and live:
+            for o in live:
+                procs[o].kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+# ---- read partition ---------------------------------------------------------------------------
+def rank_batches(args, rank: int, world: int):
+    """(reads of this rank, [reads per resident batch], scaling).  Weak scaling (default): every rank
+    owns --reads reads.  Strong scaling (--global-reads G): rank r owns the global reads r, r + N, ...
+    below G, in equal batches of at most --reads reads."""
+    if args.global_reads <= 0:
+        return args.reads, [args.reads], "weak"
+    mine = max(0, (args.global_reads - rank + world - 1) // world)
+    if mine == 0:
+        return 0, [], "strong"
+    nb = (mine + args.reads - 1) // args.reads
+    base, extra = divmod(mine, nb)
+    return mine, [base + (1 if i < extra else 0) for i in range(nb)], "strong"
+
+
+# ---- CPU baselines (the oracle: test infrastructure, timed as the reference's CPU path) -----------
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+
+    return O
 
 
 def cpu_baseline(samples_per_read: int, nreads: int, seed: int):
     """Oracle (C restatement of C5.hpp:282-683 over libzstd 1.4.x) on one host thread."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
-    import _oracle as O
 
+    O = _oracle()
     L = O.oracle()
     xs = [O.synth_read(r, samples_per_read, seed=seed) for r in range(nreads)]
     cap = L.pgno_c5_bound(samples_per_read)
@@ -92,6 +173,78 @@ def cpu_baseline(samples_per_read: int, nreads: int, seed: int):
     }
 
 
+def cpu_share() -> int:
+    """Host threads this process may use: the box's CPU share (OMP_NUM_THREADS is set to it on the
+    GPU boxes), else the affinity mask."""
+    v = os.environ.get("OMP_NUM_THREADS")
+    if v and v.isdigit() and int(v) > 0:
+        return int(v)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline_all_cores(samples_per_read: int, reads_per_thread: int, seed: int, threads: int):
+    """The same oracle path on `threads` host threads, reads sharded round-robin (ctypes releases the
+    GIL inside the C calls).  Encode and decode phases are timed separately, each from a barrier."""
+    import numpy as np
+
+    O = _oracle()
+    L = O.oracle()
+    cap = L.pgno_c5_bound(samples_per_read)
+    xs = [None] * threads
+    blobs = [[None] * reads_per_thread for _ in range(threads)]
+    bar = threading.Barrier(threads + 1)
+    errors = []
+
+    def work(t):
+        try:
+            # this thread's reads t, t + threads, ... (generated here, outside the timed phases)
+            xs[t] = [O.synth_read(t + threads * k, samples_per_read, seed=seed) for k in range(reads_per_thread)]
+            out = np.zeros(cap, np.uint8)
+            back = np.zeros(samples_per_read, np.int16)
+            ol = C.c_size_t(0)
+            bar.wait()
+            for k, x in enumerate(xs[t]):
+                if L.pgno_c5_compress(x.ctypes.data, x.size, out.ctypes.data, cap, C.byref(ol), None) != 0:
+                    errors.append("encode")
+                blobs[t][k] = out[: ol.value].copy()
+            bar.wait()
+            bar.wait()
+            for b in blobs[t]:
+                if L.pgno_c5_decompress(b.ctypes.data, b.size, back.ctypes.data, samples_per_read) != 0:
+                    errors.append("decode")
+            bar.wait()
+        except threading.BrokenBarrierError:
+            errors.append("barrier")
+
+    ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for th in ths:
+        th.start()
+    bar.wait()
+    t0 = time.perf_counter()
+    bar.wait()
+    t1 = time.perf_counter()
+    bar.wait()
+    t2 = time.perf_counter()
+    bar.wait()
+    t3 = time.perf_counter()
+    for th in ths:
+        th.join()
+    assert not errors, errors
+    n = samples_per_read * reads_per_thread * threads
+    te, td = t1 - t0, t3 - t2
+    return {
+        "value": n / (te + td) / 1e6,
+        "unit": "MSamples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{threads} threads x {reads_per_thread} synthetic reads x {samples_per_read} samples, oracle C5 "
+                  f"encode {n / te / 1e6:.1f} + decode {n / td / 1e6:.1f} MS/s",
+    }
+
+
 def host_info():
     model = "unknown"
     try:
@@ -105,6 +258,7 @@ def host_info():
     return model, os.cpu_count()
 
 
+# ---- side measurements (rank 0, N = 1) --------------------------------------------------------
 def stream_copy_gbs(torch, nbytes=4 << 30, reps=5):
     """Device STREAM-copy ceiling: read + write bytes of a large device-to-device copy."""
     a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -151,169 +305,280 @@ def pcie_inclusive(torch, codec, S, seed, nreads=2000):
             "sample": f"{nreads} reads x {S} samples, pinned host buffers"}
 
 
-def main():
-    args = parse()
+def per_chunk_plugin(torch, codec, S, seed, nreads=200):
+    """The drop-in per-chunk surface as the reference's writer/reader call it (one chunk per call,
+    host memory, synchronous: pgn_compress_signal / pgn_decompress_signal)."""
+    samples, offs, counts = codec.synth_reads(nreads, S, seed=seed)
+    host = samples.cpu().numpy()
+    torch.cuda.synchronize()
+    xs = [host[r * S:(r + 1) * S] for r in range(nreads)]
+    codec.decompress_signal(codec.compress_signal(xs[0]), sample_count=S)  # warm the staging buffers
+    t0 = time.perf_counter()
+    blobs = [codec.compress_signal(x) for x in xs]
+    t1 = time.perf_counter()
+    for b in blobs:
+        codec.decompress_signal(b, sample_count=S)
+    t2 = time.perf_counter()
+    n = nreads * S
+    return {"encode_msamples_s": round(n / (t1 - t0) / 1e6, 1), "decode_msamples_s": round(n / (t2 - t1) / 1e6, 1),
+            "calls_per_s": round(nreads / (t1 - t0), 1),
+            "sample": f"{nreads} reads x {S} samples, one pgn_compress_signal / pgn_decompress_signal call each"}
+
+
+# ---- roofline traffic evidence -------------------------------------------------------------------
+def source_digest() -> str:
+    """sha256 over the kernel sources the measured library is built from (csrc/*.hip, csrc/*.h,
+    include/*.h): a traffic file measured on other sources is stale."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "rawnanoporesignalcompression_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "rawnanoporesignalcompression_amd", "csrc", "*.h")) +
+                   glob.glob(os.path.join(ROOT, "include", "*.h")))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def load_traffic(path, R, S, dominant, applicable):
+    """(bytes per launch of the dominant direction, provenance) from the committed PMC summary, or
+    (None, reason) when it does not apply to this run or was measured on other kernel sources."""
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, f"no traffic file {os.path.relpath(path, ROOT)}"
+    if not applicable or tj.get("reads") != R or tj.get("samples") != S:
+        return None, "traffic file measured on another workload"
+    if tj.get("source_sha256") != source_digest():
+        return None, "stale: traffic file measured on other kernel sources"
+    return tj.get(dominant), os.path.relpath(path, ROOT)
+
+
+# ---- one rank ---------------------------------------------------------------------------------
+def run_rank(args, rank, world, local, codec, torch, dist, device="cuda", cuda=True):
+    """The timed body of one rank: generate this rank's reads (resident), warm up, time exactly
+    --steps steps between barriers + device synchronisation, reduce counters (SUM) and time (MAX)
+    over the ranks.  Returns the bench line on rank 0, else None.  `codec` is the device codec
+    (PGNanoCodec); the CPU tests pass a stand-in with the same methods."""
+    from rawnanoporesignalcompression_amd.shard import reduce_run, shard_reads
+
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    S = args.samples
+    mine, batches, scaling = rank_batches(args, rank, world)
+    B = max(batches) if batches else 0
+    sh = shard_reads(B, rank, world)
+    samples = torch.empty(max(B * S, 1), dtype=torch.int16, device=device)
+    counts = torch.full((B,), S, dtype=torch.int32, device=device)
+    offs = torch.arange(B, dtype=torch.int64, device=device) * S
+    if B and args.mixed_pores:  # thirds of the shard per chemistry
+        cuts = [0, B // 3, 2 * B // 3, B]
+        for i, pore in enumerate(("r941", "r103", "r1041")):
+            a, b = cuts[i], cuts[i + 1]
+            codec.synth_reads(b - a, S, seed=args.seed, first_read=sh.first_read + a * sh.read_stride,
+                              read_stride=sh.read_stride, p_switch_q16=PORES[pore], out=samples[a * S:b * S])
+    elif B:
+        codec.synth_reads(B, S, seed=args.seed, first_read=sh.first_read, read_stride=sh.read_stride,
+                          p_switch_q16=PORES[args.pore], out=samples)
+    sync()
+    caps = torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
+    boffs = torch.zeros(B, dtype=torch.int64, device=device)
+    if B > 1:
+        boffs[1:] = torch.cumsum(caps, 0)[:-1]
+    blobs = torch.empty(max(int(caps.sum().item()), 1), dtype=torch.uint8, device=device)
+    decoded = torch.empty(max(B * S, 1), dtype=torch.int16, device=device)
+    enc_ms, dec_ms = [], []
+    state = {}
+
+    def encode(nb):
+        return codec.compress_batch(samples[: nb * S], offs[:nb], counts[:nb], out=blobs, out_offsets=boffs[:nb],
+                                    out_caps=caps[:nb], stream=codec.stream)
+
+    def decode(nb, sizes):
+        codec.decompress_batch(blobs, boffs[:nb], sizes, counts[:nb], out=decoded, out_offsets=offs[:nb],
+                               stream=codec.stream)
+
+    if args.decode_only and B:  # configs[4]: the blobs are made once, outside the timed region
+        state["enc0"] = encode(B)
+        sync()
+
+    def step(timed):
+        e = d = 0.0
+        for nb in batches:
+            if args.decode_only:
+                enc = state["enc0"]
+                decode(nb, enc.sizes[:nb])
+                d += codec.last_decode_ms()
+            else:
+                enc = encode(nb)
+                decode(nb, enc.sizes)
+                e += codec.last_encode_ms()
+                d += codec.last_decode_ms()
+            state["enc"] = enc
+        if timed:
+            enc_ms.append(e)
+            dec_ms.append(d)
+
+    for _ in range(args.warmup):
+        step(False)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    # correctness of the timed work (outside the timed region): the last batch round-trips
+    ok, comp_bytes, last = True, 0, batches[-1] if batches else 0
+    if last:
+        enc = state["enc"]
+        ok = bool((enc.status[:last] == 0).all().item()) and bool(torch.equal(decoded[: last * S], samples[: last * S]))
+        comp_bytes = int(enc.sizes[:last].sum().item())
+    # bytes per sample of this rank's reads (every batch encodes reads of the same resident pool)
+    comp_rank = 0 if not last else int(round(comp_bytes * (mine * S) / (last * S)))
+    red_dev = device if (cuda and args.dist_backend == "nccl") else "cpu"
+    tot, elapsed = reduce_run({"compressed_bytes": comp_rank, "samples": mine * S, "errors": 0 if ok else 1,
+                               "chunks": mine}, elapsed, device=red_dev)
+    if rank != 0:
+        return None
+    comp_total, samples_total, errors = tot["compressed_bytes"], tot["samples"], tot["errors"]
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = samples_total * args.steps / elapsed / 1e6
+    c_per_sample = comp_total / max(samples_total, 1)
+    e_ms = sum(enc_ms) / len(enc_ms)
+    d_ms = sum(dec_ms) / len(dec_ms)
+    # the roofline is taken over the dominant direction's launch sequence (HIP events on the codec
+    # stream around all its kernels) of this rank's first batch
+    R0 = batches[0] if batches else 0
+    dominant = "c5_decode" if (d_ms >= e_ms or args.decode_only) else "c5_encode"
+    kernels = codec.kernels(1 if dominant == "c5_decode" else 0)
+    k_ms = (d_ms if args.decode_only else max(e_ms, d_ms)) / max(len(batches), 1) if batches else 0.0
+    algo_bytes = (2.0 + c_per_sample) * R0 * S  # per launch (SURVEY 8d: encode 2 + C, decode C + 2 per sample)
+    achieved = algo_bytes / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
+    traffic, traffic_src = load_traffic(args.traffic_json, R0, S, dominant,
+                                        applicable=not (args.mixed_pores or args.pore != "default" or args.decode_only))
+    if args.mixed_pores:
+        gen = "configs[4]: mixed pores (thirds R9.4.1 / R10.3 / R10.4.1 generator dwell)"
+    elif args.pore != "default":
+        gen = f"configs[2]: {args.pore} generator dwell"
+    elif args.global_reads > 0:
+        gen = f"configs[3]: {args.global_reads} global reads round-robin over {world} GPU(s)"
+    else:
+        gen = "configs[1]"
+    what = "C5 decode only" if args.decode_only else "C5 encode+decode"
+    if args.global_reads > 0:
+        shape = (f"{gen}: {args.global_reads} reads x {S} int16 samples in total (1 chunk each), resident batches "
+                 f"of <= {args.reads} reads per GPU, {what}")
+    else:
+        shape = f"{gen}: {args.reads} reads x {S} int16 samples per GPU (1 chunk each), {what}"
+    data = "synthetic (device generator: piecewise-constant levels + N(0,12) noise, integer-only)"
+    if len(batches) > 1:
+        data += "; a rank's later batches re-encode its resident pool of generated reads"
+    return {
+        "metric": METRIC if not args.decode_only else "MSamples/s decode (configs[4]); % HBM roofline",
+        "value": round(value, 2),
+        "unit": "MSamples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": scaling,
+        "vs_baseline": None,
+        "dtype": "int16",
+        "data": data,
+        "config": {
+            "workload": shape,
+            "reads_per_gpu": mine,
+            "samples_per_read": S,
+            "global_reads": samples_total // max(S, 1),
+            "parallelism": f"dp{world} (reads round-robin, no data-path collective)",
+        },
+        "encode_ms": round(e_ms, 3),
+        "decode_ms": round(d_ms, 3),
+        "encode_msamples_s": round(mine * S / e_ms / 1e3, 1) if e_ms > 0 else None,
+        "decode_msamples_s": round(mine * S / d_ms / 1e3, 1) if d_ms > 0 else None,
+        "bits_per_sample": round(8.0 * c_per_sample, 4),
+        "compressed_bytes": comp_total,
+        "round_trip_ok": errors == 0,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dominant,
+            "kernels": kernels,
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+        },
+    }
+
+
+def main(argv=None):
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` outside torchrun: start the N ranks here, before anything touches the GPU
+        sys.exit(launch_workers(args.gpus, sys.argv[1:] if argv is None else list(argv)))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus not in (1, world):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    ndev = torch.cuda.device_count()
+    dev_index = local % max(ndev, 1)  # gloo rehearsals may put several ranks on one GPU
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(dev_index)
     from rawnanoporesignalcompression_amd import PGNanoCodec
-    from rawnanoporesignalcompression_amd.shard import reduce_run, shard_reads
 
-    codec = PGNanoCodec(local)
-    R, S = args.reads, args.samples
+    codec = PGNanoCodec(dev_index)
     side = {}
     if rank == 0 and world == 1 and not args.no_side:
         side["stream_copy_gbs"] = round(stream_copy_gbs(torch), 1)
-        side["pcie_inclusive"] = pcie_inclusive(torch, codec, S, args.seed)
-    # this rank's shard: global reads rank, rank + world, ... (round-robin)
-    sh = shard_reads(R, rank, world)
-    samples = torch.empty(R * S, dtype=torch.int16, device="cuda")
-    counts = torch.full((R,), S, dtype=torch.int32, device="cuda")
-    offs = torch.arange(R, dtype=torch.int64, device="cuda") * S
-    if args.mixed_pores:  # thirds of the shard per chemistry
-        cuts = [0, R // 3, 2 * R // 3, R]
-        for i, pore in enumerate(("r941", "r103", "r1041")):
-            a, b = cuts[i], cuts[i + 1]
-            codec.synth_reads(b - a, S, seed=args.seed, first_read=sh.first_read + a * sh.read_stride,
-                              read_stride=sh.read_stride, p_switch_q16=PORES[pore], out=samples[a * S:b * S])
-    else:
-        codec.synth_reads(R, S, seed=args.seed, first_read=sh.first_read, read_stride=sh.read_stride,
-                          p_switch_q16=PORES[args.pore], out=samples)
-    torch.cuda.synchronize()
-    caps = torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
-    boffs = torch.zeros(R, dtype=torch.int64, device="cuda")
-    boffs[1:] = torch.cumsum(caps, 0)[:-1]
-    blobs = torch.empty(int(caps.sum().item()), dtype=torch.uint8, device="cuda")
-    decoded = torch.empty(R * S, dtype=torch.int16, device="cuda")
-
-    def step():
-        enc = codec.compress_batch(samples, offs, counts, out=blobs, out_offsets=boffs, out_caps=caps,
-                                   stream=codec.stream)
-        codec.decompress_batch(blobs, boffs, enc.sizes, counts, out=decoded, out_offsets=offs,
-                               stream=codec.stream)
-        return enc
-
-    if args.decode_only:  # configs[4]: the blobs are made once, outside the timed region
-        enc0 = codec.compress_batch(samples, offs, counts, out=blobs, out_offsets=boffs, out_caps=caps,
-                                    stream=codec.stream)
-        torch.cuda.synchronize()
-
-        def step():  # noqa: F811
-            codec.decompress_batch(blobs, boffs, enc0.sizes, counts, out=decoded, out_offsets=offs,
-                                   stream=codec.stream)
-            return enc0
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    enc_ms, dec_ms = [], []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        enc = step()
-        enc_ms.append(codec.last_encode_ms())
-        dec_ms.append(codec.last_decode_ms())
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    # correctness of the timed work (outside the timed region)
-    ok = bool((enc.status == 0).all().item()) and bool(torch.equal(decoded, samples))
-    comp_bytes = int(enc.sizes.sum().item())
-    # the final size/ratio reduction (RCCL over xGMI) and the max-over-ranks time
-    tot, elapsed = reduce_run({"compressed_bytes": comp_bytes, "samples": R * S, "errors": 0 if ok else 1,
-                               "chunks": R}, elapsed, device="cuda")
-    comp_total, samples_total, errors = tot["compressed_bytes"], tot["samples"], tot["errors"]
-    if rank == 0:
-        ms_per_step = 1e3 * elapsed / args.steps
-        value = samples_total * args.steps / elapsed / 1e6
-        c_per_sample = comp_total / samples_total
-        e_ms = sum(enc_ms) / len(enc_ms)
-        d_ms = sum(dec_ms) / len(dec_ms)
-        # the hot path is a three-kernel pipeline per direction; the roofline is taken over the dominant
-        # direction's launch sequence (HIP events on the codec stream around all its kernels)
-        dominant = "c5_decode" if (d_ms >= e_ms or args.decode_only) else "c5_encode"
-        kernels = codec.kernels(1 if dominant == "c5_decode" else 0)
-        k_ms = d_ms if args.decode_only else max(e_ms, d_ms)
-        algo_bytes = (2.0 + comp_bytes / (R * S)) * R * S  # per launch on this GPU
-        achieved = algo_bytes / (k_ms * 1e-3) / 1e9
-        traffic = None
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("reads") == R and tj.get("samples") == S and not (args.mixed_pores or args.pore != "default"):
-                traffic = tj.get(dominant)
-        except (OSError, ValueError):
-            pass
-        if args.mixed_pores:
-            gen = "configs[4]: mixed pores (thirds R9.4.1 / R10.3 / R10.4.1 generator dwell)"
-        elif args.pore != "default":
-            gen = f"configs[2]: {args.pore} generator dwell"
-        else:
-            gen = "configs[1]"
-        what = "C5 decode only" if args.decode_only else "C5 encode+decode"
-        line = {
-            "metric": METRIC if not args.decode_only else "MSamples/s decode (configs[4]); % HBM roofline",
-            "value": round(value, 2),
-            "unit": "MSamples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int16",
-            "data": "synthetic (device generator: piecewise-constant levels + N(0,12) noise, integer-only)",
-            "config": {
-                "workload": f"{gen}: {R} reads x {S} int16 samples per GPU (1 chunk each), {what}",
-                "reads_per_gpu": R,
-                "samples_per_read": S,
-                "parallelism": f"dp{world} (reads round-robin, no data-path collective)",
-            },
-            "encode_ms": round(e_ms, 3),
-            "decode_ms": round(d_ms, 3),
-            "encode_msamples_s": round(R * S / e_ms / 1e3, 1),
-            "decode_msamples_s": round(R * S / d_ms / 1e3, 1),
-            "bits_per_sample": round(8.0 * c_per_sample, 4),
-            "round_trip_ok": errors == 0,
-            "roofline": {
-                "bound": "hbm",
-                "kernel": dominant,
-                "kernels": kernels,
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-            },
-        }
+        side["pcie_inclusive"] = pcie_inclusive(torch, codec, args.samples, args.seed)
+        side["per_chunk_plugin"] = per_chunk_plugin(torch, codec, args.samples, args.seed)
+    line = run_rank(args, rank, world, local, codec, torch, dist, device=torch.device("cuda", dev_index))
+    if line is not None:
         line.update(side)
+        R, S = args.reads, args.samples
         if args.compare_vbz and world == 1:  # the --VBZ side of the ratio comparison, outside the timing
             from rawnanoporesignalcompression_amd import VBZCodec
 
-            vz = VBZCodec(local)
+            samples = torch.empty(R * S, dtype=torch.int16, device="cuda")
+            _, offs, counts = codec.synth_reads(R, S, seed=args.seed, p_switch_q16=PORES[args.pore], out=samples)
+            vz = VBZCodec(dev_index)
             ev = vz.compress_batch(samples, offs, counts)
             torch.cuda.synchronize()
             vbytes = int(ev.sizes.sum().item())
+            c5bytes = line["compressed_bytes"]
             line["vbz"] = {"bits_per_sample": round(8.0 * vbytes / (R * S), 4),
-                           "c5_vs_vbz_ratio": round(comp_bytes / max(vbytes, 1), 4),
+                           "c5_vs_vbz_ratio": round(c5bytes / max(vbytes, 1), 4),
                            "status_ok": bool((ev.status == 0).all().item())}
             vz.close()
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(S, args.cpu_sample_reads, args.seed) if world == 1 else None
-            if line["cpu_baseline"]:
-                model, ncpu = host_info()
-                line["cpu_baseline"]["sample"] += f"; host {model}, {ncpu} logical CPUs"
+            del samples
+        if not args.no_cpu_baseline and world == 1:
+            model, ncpu = host_info()
+            line["cpu_baseline"] = cpu_baseline(S, args.cpu_sample_reads, args.seed)
+            line["cpu_baseline"]["sample"] += f"; host {model}, {ncpu} logical CPUs"
+            threads = args.cpu_threads or cpu_share()
+            line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(S, max(8, 4 * args.cpu_sample_reads // threads),
+                                                                    args.seed, threads)
+            line["cpu_baseline_all_cores"]["sample"] += f"; host {model}, {ncpu} logical CPUs, CPU share {threads}"
+        elif not args.no_cpu_baseline:
+            line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -77,6 +77,17 @@ int pgn_decompress_signal(pgn_ctx *ctx, const uint8_t *compressed, size_t compre
 int pgn_pinanoraw_compress_signal(const int16_t *signal, size_t signal_size, char *compressed_signal_out,
                                   size_t *compressed_signal_size);
 
+/* pod5_vbz_compress_signal / pod5_vbz_decompress_signal (c_api.h:685-711, c_api.cpp:1183-1214,
+ * 1255-1273) with the same argument shapes, on the default context of device 0: the VBZ codec of
+ * the reference's --VBZ path.  Compress: *compressed_signal_size is the buffer size on input and
+ * the blob size on output (a blob larger than the buffer is PGN_ERR_DST_TOO_SMALL, the reference's
+ * "Compressed signal size (..) is greater than provided buffer size").  Decompress: sample_count
+ * samples into signal_out. */
+int pgn_pod5_vbz_compress_signal(const int16_t *signal, size_t signal_size, char *compressed_signal_out,
+                                 size_t *compressed_signal_size);
+int pgn_pod5_vbz_decompress_signal(const char *compressed_signal, size_t compressed_signal_size,
+                                   size_t sample_count, short *signal_out);
+
 /* Batched, device-resident encode of `nchunks` independent chunks (each <= PGN_MAX_CHUNK_SAMPLES):
  * chunk i = d_samples[d_sample_offsets[i] .. + d_sample_counts[i]) -> d_out[d_out_offsets[i] ..),
  * capacity d_out_caps[i]; d_out_sizes[i] and d_status[i] receive the result.  d_stats (optional)

@@ -15,7 +15,9 @@ from .codec import (
     decompress_signal,
     default_codec,
     pinanoraw_compress_signal,
+    vbz_compress_signal_capi,
     vbz_compressed_signal_max_size,
+    vbz_decompress_signal_capi,
 )
 
 __all__ = [
@@ -31,5 +33,7 @@ __all__ = [
     "default_codec",
     "load_native",
     "pinanoraw_compress_signal",
+    "vbz_compress_signal_capi",
     "vbz_compressed_signal_max_size",
+    "vbz_decompress_signal_capi",
 ]

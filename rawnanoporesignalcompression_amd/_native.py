@@ -43,6 +43,8 @@ SIGNATURES = [
     ("pgn_compress_signal", C.c_int, [_VP, _VP, _SZ, _VP, _SZ, C.POINTER(C.c_size_t)]),
     ("pgn_decompress_signal", C.c_int, [_VP, _VP, _SZ, _VP, _SZ]),
     ("pgn_pinanoraw_compress_signal", C.c_int, [_VP, _SZ, _VP, C.POINTER(C.c_size_t)]),
+    ("pgn_pod5_vbz_compress_signal", C.c_int, [_VP, _SZ, _VP, C.POINTER(C.c_size_t)]),
+    ("pgn_pod5_vbz_decompress_signal", C.c_int, [_VP, _SZ, _SZ, _VP]),
     ("pgn_compress_batch_device", C.c_int,
      [_VP, _SZ, _VP, _U64P, _U32P, _VP, _U64P, _U64P, _U64P, _I32P, _U64P, _VP]),
     ("pgn_decompress_batch_device", C.c_int, [_VP, _SZ, _VP, _U64P, _U64P, _VP, _U64P, _U32P, _I32P, _VP]),

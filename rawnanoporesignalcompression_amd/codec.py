@@ -59,6 +59,12 @@ def _ptr(t) -> int:
     return t.data_ptr() if t is not None else 0
 
 
+def _require_device(t, name: str, device: int) -> None:
+    """The batch kernels dereference their data pointers on the GPU: a host tensor would fault."""
+    if not t.is_cuda or t.device.index != device:
+        raise ValueError(f"{name} must be a tensor on cuda:{device} (got {t.device})")
+
+
 @dataclass
 class EncodedBatch:
     blobs: "object"          # torch.uint8 device tensor holding every blob at its offset
@@ -170,6 +176,9 @@ class PGNanoCodec:
         """
         import torch
 
+        _require_device(samples, "samples", self.device)
+        if out is not None:
+            _require_device(out, "out", self.device)
         caller = torch.cuda.current_stream()
         ls = self._launch_stream(stream)
         with torch.cuda.stream(ls):
@@ -204,6 +213,9 @@ class PGNanoCodec:
         """Decode a device-resident batch; returns (samples int16 tensor, offsets, status)."""
         import torch
 
+        _require_device(blobs, "blobs", self.device)
+        if out is not None:
+            _require_device(out, "out", self.device)
         caller = torch.cuda.current_stream()
         ls = self._launch_stream(stream)
         with torch.cuda.stream(ls):
@@ -219,11 +231,12 @@ class PGNanoCodec:
             if out is None:
                 total = int(counts.to(torch.int64).sum().item())
                 out = torch.empty(max(total, 1), dtype=torch.int16, device=dev)
+            bo = blob_offsets.to(device=dev, dtype=torch.int64).contiguous()
+            bs = blob_sizes.to(device=dev, dtype=torch.int64).contiguous()
             status = torch.full((n,), -1, dtype=torch.int32, device=dev)
             _check(self._call(
-                self._fn_decompress_batch, n, _ptr(blobs), _ptr(blob_offsets.to(torch.int64).contiguous()),
-                _ptr(blob_sizes.to(torch.int64).contiguous()), _ptr(out), _ptr(so), _ptr(counts), _ptr(status),
-                ls.cuda_stream))
+                self._fn_decompress_batch, n, _ptr(blobs), _ptr(bo), _ptr(bs), _ptr(out), _ptr(so), _ptr(counts),
+                _ptr(status), ls.cuda_stream))
         caller.wait_stream(ls)
         return out, so, status
 
@@ -318,3 +331,24 @@ def pinanoraw_compress_signal(signal, buffer_size: int | None = None) -> bytes:
     size = C.c_size_t(cap)
     _check(lib.pgn_pinanoraw_compress_signal(x.ctypes.data, x.size, out.ctypes.data, C.byref(size)))
     return out[: size.value].tobytes()
+
+
+def vbz_compress_signal_capi(signal, buffer_size: int | None = None) -> bytes:
+    """``pod5_vbz_compress_signal`` (c_api.cpp:1183-1214): the --VBZ codec through the C-API shape."""
+    lib = _native.load()
+    x = np.ascontiguousarray(signal, dtype=np.int16)
+    cap = buffer_size if buffer_size is not None else vbz_compressed_signal_max_size(x.size)
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    size = C.c_size_t(cap)
+    _check(lib.pgn_pod5_vbz_compress_signal(x.ctypes.data, x.size, out.ctypes.data, C.byref(size)))
+    return out[: size.value].tobytes()
+
+
+def vbz_decompress_signal_capi(compressed, sample_count: int):
+    """``pod5_vbz_decompress_signal`` (c_api.cpp:1255-1273)."""
+    lib = _native.load()
+    src = np.frombuffer(bytes(compressed), dtype=np.uint8)
+    out = np.empty(max(int(sample_count), 1), dtype=np.int16)
+    _check(lib.pgn_pod5_vbz_decompress_signal(src.ctypes.data if src.size else 0, src.size, int(sample_count),
+                                              out.ctypes.data))
+    return out[: int(sample_count)]

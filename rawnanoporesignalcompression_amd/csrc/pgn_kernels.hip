@@ -970,6 +970,12 @@ struct pgn_ctx {
     hipEvent_t evFork = nullptr, evJoin = nullptr, evStage[2] = {nullptr, nullptr}, evFree[2] = {nullptr, nullptr};
     uint64_t* prof = nullptr;  // [2][kPhases] phase cycles (encode, decode) when PGN_PHASE_PROFILE=1
     bool encTimed = false, decTimed = false;
+    // Stream ordering of the context's shared state (work counters, slot scratch, per-chunk buffers):
+    // every launch sequence records evLast on its stream at the end, and the next one, on whatever
+    // stream, waits for it before touching that state.  Calls on one context therefore run in call
+    // order on the device even when callers pass different streams.
+    hipEvent_t evLast = nullptr;
+    bool haveLast = false;
     std::mutex mu;
 };
 
@@ -1060,6 +1066,7 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         HIPCHK(hipDeviceSynchronize());
     }
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    HIPCHK(hipEventCreateWithFlags(&c->evLast, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming));
@@ -1090,7 +1097,8 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->prof);
     for (int i = 0; i < 4; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->side) (void)hipStreamSynchronize(c->side);
-    for (hipEvent_t e : {c->evFork, c->evJoin, c->evStage[0], c->evStage[1], c->evFree[0], c->evFree[1]})
+    if (c->evLast) (void)hipEventSynchronize(c->evLast);
+    for (hipEvent_t e : {c->evFork, c->evJoin, c->evStage[0], c->evStage[1], c->evFree[0], c->evFree[1], c->evLast})
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->stream);
@@ -1100,10 +1108,17 @@ int pgn_ctx_destroy(pgn_ctx* c)
 
 void* pgn_ctx_stream(pgn_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
+// The last launch sequence on any stream (evLast) has finished with the context's buffers.
+static void wait_last_host(pgn_ctx* c)
+{
+    if (c->haveLast) (void)hipEventSynchronize(c->evLast);
+    (void)hipStreamSynchronize(c->stream);
+}
+
 static int ensure_enc(pgn_ctx* c, size_t slots, size_t G)
 {
     if (slots > c->encSlots) {
-        (void)hipStreamSynchronize(c->stream);
+        wait_last_host(c);
         (void)hipFree(c->encScratch);
         (void)hipFree(c->epochs);
         c->encScratch = nullptr;
@@ -1119,6 +1134,7 @@ static int ensure_enc(pgn_ctx* c, size_t slots, size_t G)
         c->encSlots = slots;
     }
     if (G > c->encG) {  // G = chunk capacity over all buffers
+        wait_last_host(c);
         (void)hipDeviceSynchronize();
         (void)hipFree(c->encChunks);
         c->encChunks = nullptr;
@@ -1131,13 +1147,14 @@ static int ensure_enc(pgn_ctx* c, size_t slots, size_t G)
 static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
 {
     if (slots > c->decSlots) {
-        (void)hipStreamSynchronize(c->stream);
+        wait_last_host(c);
         (void)hipFree(c->decScratch);
         c->decScratch = nullptr;
         HIPCHK(hipMalloc(&c->decScratch, dec_slot_bytes() * slots));
         c->decSlots = slots;
     }
     if (G > c->decG) {  // G = chunk capacity over all buffers
+        wait_last_host(c);
         (void)hipDeviceSynchronize();
         (void)hipFree(c->decChunks);
         c->decChunks = nullptr;
@@ -1150,7 +1167,7 @@ static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
 static int ensure_queues(pgn_ctx* c, size_t n, hipStream_t s)
 {
     if (n > c->nQueues) {
-        (void)hipStreamSynchronize(c->stream);
+        wait_last_host(c);
         (void)hipStreamSynchronize(s);
         (void)hipFree(c->queues);
         c->queues = nullptr;
@@ -1245,7 +1262,7 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     return PGN_OK;
 }
 
-static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
+static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
                          const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
                          const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
                          void* stream)
@@ -1313,7 +1330,7 @@ static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d
     return PGN_OK;
 }
 
-static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
+static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
                          const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
                          const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
 {
@@ -1376,6 +1393,37 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     HIPCHK(hipEventRecord(c->ev[3], s));
     c->decTimed = true;
     return PGN_OK;
+}
+
+// Every launch sequence on a context: ordered after the previous one (evLast, whatever its stream),
+// and recorded as the new last one.
+static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
+                         const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
+                         const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
+                         void* stream)
+{
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (c->haveLast) HIPCHK(hipStreamWaitEvent(s, c->evLast, 0));
+    const int rc = launch_encode_impl(c, codec, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out,
+                                      d_out_offsets, d_out_caps, d_out_sizes, d_status, d_stats, s);
+    HIPCHK(hipEventRecord(c->evLast, s));
+    c->haveLast = true;
+    return rc;
+}
+
+static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
+                         const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
+                         const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
+{
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    if (c->haveLast) HIPCHK(hipStreamWaitEvent(s, c->evLast, 0));
+    const int rc = launch_decode_impl(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                                      d_sample_counts, d_status, s);
+    HIPCHK(hipEventRecord(c->evLast, s));
+    c->haveLast = true;
+    return rc;
 }
 
 static int compress_batch(int codec, pgn_ctx* c, size_t nchunks, const int16_t* d_samples,
@@ -1697,22 +1745,33 @@ int pgn_variant_decompress_signal(pgn_ctx* c, int variant, const uint8_t* src, s
 static pgn_ctx* g_default = nullptr;
 static std::mutex g_default_mu;
 
-int pgn_pinanoraw_compress_signal(const int16_t* signal, size_t signal_size, char* out, size_t* inout_size)
+static int default_ctx(pgn_ctx** c)
+{
+    std::lock_guard<std::mutex> g(g_default_mu);
+    if (!g_default) {
+        const int rc = pgn_ctx_create(0, &g_default);
+        if (rc) return rc;
+    }
+    *c = g_default;
+    return PGN_OK;
+}
+
+// The pod5 C-API wrappers (c_api.cpp:1183-1253): compress into a buffer of the codec's maximum size,
+// then check the caller's buffer ("Compressed signal size (..) is greater than provided buffer size").
+static int capi_compress(int codec, const int16_t* signal, size_t signal_size, char* out, size_t* inout_size)
 {
     if (!signal || !out || !inout_size) return PGN_ERR_INVALID_ARG;
-    {
-        std::lock_guard<std::mutex> g(g_default_mu);
-        if (!g_default) {
-            int rc = pgn_ctx_create(0, &g_default);
-            if (rc) return rc;
-        }
-    }
-    // pgnano::compress_signal allocates compressed_signal_max_size(n) (pgnano.cpp:66-68) ...
-    const size_t cap = pgn_compressed_signal_max_size(signal_size);
+    pgn_ctx* c = nullptr;
+    int rc = default_ctx(&c);
+    if (rc) return rc;
+    // pgnano::compress_signal allocates compressed_signal_max_size(n) (pgnano.cpp:66-68), pod5's
+    // VBZ compress_signal pod5::compressed_signal_max_size(n) (signal_compression.cpp:21-35) ...
+    const size_t cap = codec == kCodecVbz ? pgn_vbz_compressed_signal_max_size(signal_size)
+                                          : pgn_compressed_signal_max_size(signal_size);
     uint8_t* tmp = (uint8_t*)malloc(cap);
     if (!tmp) return PGN_ERR_INVALID_ARG;
     size_t sz = 0;
-    int rc = pgn_compress_signal(g_default, signal, signal_size, tmp, cap, &sz);
+    rc = compress_signal(codec, c, signal, signal_size, tmp, cap, &sz);
     if (rc == PGN_OK) {
         // ... then c_api.cpp:1240-1250 checks the caller's buffer
         if (sz > *inout_size) {
@@ -1724,6 +1783,25 @@ int pgn_pinanoraw_compress_signal(const int16_t* signal, size_t signal_size, cha
     }
     free(tmp);
     return rc;
+}
+
+int pgn_pinanoraw_compress_signal(const int16_t* signal, size_t signal_size, char* out, size_t* inout_size)
+{
+    return capi_compress(kCodecC5, signal, signal_size, out, inout_size);
+}
+
+int pgn_pod5_vbz_compress_signal(const int16_t* signal, size_t signal_size, char* out, size_t* inout_size)
+{
+    return capi_compress(kCodecVbz, signal, signal_size, out, inout_size);
+}
+
+int pgn_pod5_vbz_decompress_signal(const char* compressed, size_t compressed_size, size_t sample_count, short* out)
+{
+    if (!compressed || !out) return PGN_ERR_INVALID_ARG;  // check_not_null / check_output_pointer_not_null
+    pgn_ctx* c = nullptr;
+    const int rc = default_ctx(&c);
+    if (rc) return rc;
+    return decompress_signal(kCodecVbz, c, (const uint8_t*)compressed, compressed_size, (int16_t*)out, sample_count);
 }
 
 }  // extern "C"

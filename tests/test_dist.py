@@ -71,3 +71,98 @@ def test_shard_validation():
     assert s.global_ids() == [1, 4, 7, 10]
     with pytest.raises(ValueError):
         shard_reads(4, 3, 3)
+
+
+# ---- bench.py's own orchestration under gloo (CPU stand-in codec) ------------------------------
+def _bench_worker(rank, world, port, argv, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from _cpu_codec import CpuCodec
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    args = bench.parse(argv)
+    line = bench.run_rank(args, rank, world, rank, CpuCodec(), torch, dist, device="cpu", cuda=False)
+    q.put((rank, line))
+    dist.destroy_process_group()
+
+
+def _run_bench_ranks(world, argv):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, argv, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_bench_rank_body_weak_scaling_two_ranks():
+    """bench.run_rank on two gloo ranks: round-robin shards, barriers, SUM/MAX reduction, the line."""
+    import _oracle as O
+
+    reads, n = 3, 2000
+    res = _run_bench_ranks(2, ["--gpus", "2", "--reads", str(reads), "--samples", str(n), "--steps", "1",
+                               "--warmup", "0", "--no-side", "--no-cpu-baseline"])
+    assert res[1] is None
+    line = res[0]
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and line["round_trip_ok"]
+    assert line["config"]["global_reads"] == 2 * reads
+    want = sum(len(O.c5_compress(O.synth_read(g, n))[1]) for g in range(2 * reads))
+    assert line["compressed_bytes"] == want
+    assert line["value"] > 0 and line["roofline"]["traffic"] is None
+
+
+def test_bench_rank_body_strong_scaling_batches():
+    """--global-reads: a fixed read set split round-robin over the ranks, in resident batches."""
+    reads_total, n = 7, 1500
+    res = _run_bench_ranks(2, ["--global-reads", str(reads_total), "--reads", "2", "--samples", str(n),
+                               "--steps", "1", "--warmup", "0", "--no-side", "--no-cpu-baseline"])
+    line = res[0]
+    assert line["scaling"] == "strong" and line["round_trip_ok"]
+    assert line["config"]["global_reads"] == reads_total
+    assert line["config"]["reads_per_gpu"] == 4  # rank 0 owns reads 0, 2, 4, 6
+
+
+def test_rank_batches_partition():
+    import bench
+
+    for G, world, B in [(1_000_000, 8, 100_000), (1_000_000, 1, 100_000), (7, 3, 2), (5, 8, 4)]:
+        args = bench.parse(["--global-reads", str(G), "--reads", str(B)])
+        tot = 0
+        for r in range(world):
+            mine, batches, scaling = bench.rank_batches(args, r, world)
+            assert scaling == "strong" and sum(batches) == mine and all(0 < b <= B for b in batches)
+            assert mine == len(range(r, G, world))
+            tot += mine
+        assert tot == G
+    mine, batches, scaling = bench.rank_batches(bench.parse([]), 0, 4)
+    assert (mine, batches, scaling) == (100_000, [100_000], "weak")
+
+
+def test_launcher_gives_each_rank_torchrun_env(tmp_path):
+    """bench.py --gpus N outside torchrun: N worker processes with RANK/LOCAL_RANK/WORLD_SIZE and a
+    127.0.0.1 rendezvous; a failing rank makes the launch fail."""
+    import json
+
+    import bench
+
+    probe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_rank_probe.py")
+    assert bench.launch_workers(3, [str(tmp_path), "-1"], script=probe, timeout=120) == 0
+    envs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(3)]
+    assert [e["RANK"] for e in envs] == ["0", "1", "2"] and [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
+    assert {e["WORLD_SIZE"] for e in envs} == {"3"} and {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
+    assert len({e["MASTER_PORT"] for e in envs}) == 1
+    assert bench.launch_workers(2, [str(tmp_path), "1"], script=probe, timeout=120) == 3

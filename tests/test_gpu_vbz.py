@@ -152,3 +152,18 @@ def test_full_size_chunks_round_trip(vbz):
     bo, bs = enc.offsets.cpu().numpy(), enc.sizes.cpu().numpy()
     for r in list(range(0, k, 127)) + [k - 1]:
         assert blobs[bo[r]:bo[r] + bs[r]].tobytes() == O.vbz_compress(O.synth_read(r, n)), r
+
+
+def test_pod5_c_api_shapes(vbz):
+    """pod5_vbz_compress_signal / pod5_vbz_decompress_signal (c_api.cpp:1183-1273) through their
+    same-shape exports: fixture blobs reproduced, a too-small buffer refused with the blob size."""
+    from rawnanoporesignalcompression_amd import PGNanoError
+    from rawnanoporesignalcompression_amd.codec import vbz_compress_signal_capi, vbz_decompress_signal_capi
+
+    for i, (blob, n) in enumerate(real_vbz_chunks()[:6]):
+        x = vbz_decompress_signal_capi(blob, n)
+        assert np.array_equal(x, O.vbz_decompress(blob, n)[1]), i
+        assert vbz_compress_signal_capi(x) == blob, i
+        with pytest.raises(PGNanoError) as ei:
+            vbz_compress_signal_capi(x, buffer_size=len(blob) - 1)
+        assert ei.value.status == 1, i

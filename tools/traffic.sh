@@ -1,5 +1,5 @@
 #!/bin/bash
-# HBM traffic of one bench step, per kernel (run on the GPU box).  Two separate --pmc passes
+# HBM traffic and L2 hit rate of one bench step, per kernel (run on the GPU box).  Separate --pmc passes
 # (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950: MI355X_MICROARCH.md "rocprofv3 PMC
 # slots"), then tools/traffic_summary.py applies the guide's gfx950 FETCH_SIZE correction and
 # writes gpurun_out/traffic_<tag>.json; copied to profiles/, bench.py reads it into roofline.traffic.
@@ -9,8 +9,10 @@ R=${2:-100000}
 S=${3:-100000}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/traffic
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/traffic/$C -o run -- \
-      python3 tools/traffic_probe.py $R $S > gpurun_out/traffic/$C.log 2>&1
+# third pass: L2 hit/miss (TCC_HIT_sum / TCC_MISS_sum, 2 of the 4 TCC slots)
+for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+  D=${C%% *}
+  timeout -s KILL 400 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/traffic/$D -o run -- \
+      python3 tools/traffic_probe.py $R $S > gpurun_out/traffic/$D.log 2>&1
 done
 python3 tools/traffic_summary.py gpurun_out/traffic $R $S gpurun_out/traffic_$TAG.json  # copied into profiles/ to commit

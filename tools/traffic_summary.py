@@ -26,14 +26,21 @@ if "enc_chunk_kernel<0>" in val:
     stages["c5_encode"] = ["enc_chunk_kernel<0>"]
 if "dec_chunk_kernel<0>" in val:
     stages["c5_decode"] = ["dec_chunk_kernel<0>"]
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import source_digest  # noqa: E402  (the kernel sources this measurement belongs to)
+
 res = {"reads": R, "samples": S, "unit": "bytes per stage launch (one direction over the whole batch)",
+       "source_sha256": source_digest(),
        "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)", "kernels": {}}
 for k, v in val.items():
     if not any(k.startswith(p) for p in ("enc_", "dec_")):
         continue
     fetch, write = v.get("FETCH_SIZE", 0.0) * 1024, v.get("WRITE_SIZE", 0.0) * 1024
+    hit, miss = v.get("TCC_HIT_sum", 0.0), v.get("TCC_MISS_sum", 0.0)
     res["kernels"][k] = {"fetch_raw": fetch, "write": write, "bytes": 2 * fetch + write,
-                         "dispatches": calls[k].get("FETCH_SIZE", 0)}
+                         "dispatches": calls[k].get("FETCH_SIZE", 0),
+                         "tcc_hit": hit, "tcc_miss": miss,
+                         "l2_hit_rate": round(hit / (hit + miss), 4) if hit + miss > 0 else None}
 for st, ks in stages.items():
     if all(k in res["kernels"] for k in ks):
         res[st] = sum(res["kernels"][k]["bytes"] for k in ks)
