@@ -85,7 +85,8 @@ def load(path: str | None = None) -> C.CDLL:
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or (PROF_LIB_PATH if os.environ.get("PGN_PHASE_PROFILE") == "1" else LIB_PATH)
+        # PGN_LIB: an alternative build of the same library (A/B measurements of kernel variants)
+        p = path or os.environ.get("PGN_LIB") or (PROF_LIB_PATH if os.environ.get("PGN_PHASE_PROFILE") == "1" else LIB_PATH)
         # One HIP runtime per process: PyTorch ships its own libamdhip64 (soname libamdhip64.so.7,
         # but its libraries NEED the unversioned name), so load torch first and let this library
         # bind to the runtime torch already mapped; loading ours first would map a second runtime.

@@ -14,12 +14,12 @@ extern "C" {
 // ZSTD_compress(dst, cap, src, n, 1) equivalent; returns size or 0 on error/unsupported.
 size_t z1m_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap)
 {
-    if (n > kMaxSrc || cap < compress_bound(n)) return 0;
+    if (n > kMaxFrameSrc || cap < compress_bound(n)) return 0;
     uint32_t* ht = (uint32_t*)calloc((size_t)1 << 15, 4);
-    size_t ns = n / 4 + 2;
+    size_t ns = kMaxSrc / 4 + 2;
     Seq* seqs = (Seq*)malloc(ns * sizeof(Seq));
     uint8_t* codes = (uint8_t*)malloc(3 * ns);
-    uint8_t* litbuf = (uint8_t*)malloc(n + 1);
+    uint8_t* litbuf = (uint8_t*)malloc(kMaxSrc + 1);
     CompressWork* w = (CompressWork*)malloc(sizeof(CompressWork));
     size_t r = compress_serial(dst, src, n, ht, seqs, codes, codes + ns, codes + 2 * ns, litbuf, *w);
     free(w); free(litbuf); free(codes); free(seqs); free(ht);
@@ -33,7 +33,8 @@ size_t z1m_sequences(const uint8_t* src, size_t n, uint32_t* out3, size_t maxSeq
     uint32_t* ht = (uint32_t*)calloc((size_t)1 << 15, 4);
     Seq* seqs = (Seq*)malloc((n / 4 + 2) * sizeof(Seq));
     size_t lastLL = 0;
-    size_t nb = fast_search_serial(src, n, level1_params(n), ht, seqs, &lastLL);
+    uint32_t rep[3] = {1, 4, 8};
+    size_t nb = fast_search_serial(src, 0, n, level1_params(n), ht, rep, seqs, &lastLL);
     for (size_t i = 0; i < nb && i < maxSeq; i++) {
         out3[3 * i] = seqs[i].litLength; out3[3 * i + 1] = seqs[i].offset; out3[3 * i + 2] = seqs[i].mlBase;
     }

@@ -74,9 +74,10 @@ __device__ __forceinline__ void stg_entry2(StgBits& r, int lane, int32_t x, uint
     e2 = sDec.tab[(uint32_t)(r.Wd >> ((x2 - r.wlo) & 63)) & tmask];
 }
 
-// Returns false on a malformed section.
+// Returns false on a malformed section.  jt = the jump table's three stream sizes (l1 | l2 << 16,
+// l3), read by the caller (remain >= 6).
 __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                              PhaseProf& P)
+                                              uint32_t jt01, uint32_t jt2, PhaseProf& P)
 {
     const int lane = lane_id();
     tl = uni(tl);
@@ -84,9 +85,10 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     remain = uni((uint64_t)remain);
     dst = uni(dst);
     rs = uni(rs);
+    jt01 = uni(jt01);
+    jt2 = uni(jt2);
     const int k = lane >> 4, j = lane & 15;
-    if (remain < 6) return false;
-    const size_t l1 = gld<uint16_t>(hp), l2 = gld<uint16_t>(hp + 2), l3 = gld<uint16_t>(hp + 4);
+    const size_t l1 = jt01 & 0xFFFFu, l2 = jt01 >> 16, l3 = jt2;
     if (l1 + l2 + l3 + 6 > remain) return false;
     const size_t l4 = remain - 6 - l1 - l2 - l3;
     const uint32_t seg = (rs + 3) / 4;

@@ -170,6 +170,21 @@ __device__ inline void wave_copy(uint8_t* dst, const uint8_t* src, size_t n)
     for (; i + 16 <= n; i += 1024) gst<uint4>(dst + i, gld<uint4>(src + i));
     for (size_t b = (n & ~(size_t)15) + (size_t)lane; b < n; b += 64) gst<uint8_t>(dst + b, gb(src + b));
 }
+// the same with eight 16-byte loads in flight per lane (8 KiB per wave round trip): large copies
+// such as a raw block are latency-bound on the number of round trips
+__device__ inline void wave_copy8(uint8_t* dst, const uint8_t* src, size_t n)
+{
+    const size_t l16 = (size_t)lane_id() * 16;
+    size_t base = 0;  // wave-uniform: whole 8 KiB rounds, then wave_copy for the rest
+    for (; base + 8192 <= n; base += 8192) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = gld<uint4>(src + base + l16 + 1024 * k);
+#pragma unroll
+        for (int k = 0; k < 8; k++) gst<uint4>(dst + base + l16 + 1024 * k, v[k]);
+    }
+    wave_copy(dst + base, src + base, n - base);
+}
 __device__ inline void wave_fill(uint8_t* dst, uint8_t v, size_t n)
 {
     for (size_t i = lane_id(); i < n; i += 64) gst<uint8_t>(dst + i, v);

@@ -37,8 +37,6 @@ struct alignas(16) DecLds {
                     uint8_t hbuf[272];        // staged Huffman table description (zero padded)
                     z1::FseDEntry wdt[64];    // weights FSE decode table (tableLog <= 6)
                     int16_t wnorm[16];
-                    uint16_t wnext[16];
-                    uint32_t wrank[16];
                 };
             };
         };
@@ -113,6 +111,50 @@ __device__ __forceinline__ uint32_t rb_huf(RevBits& r, int32_t& pos, unsigned tl
     const uint32_t e = gt ? (uint32_t)gld<uint16_t>(gt + ix) : (uint32_t)sDec.tab[ix];
     pos -= (int32_t)(e >> 8);
     return e & 0xFF;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Header window: 256 bytes of a frame held in one VGPR (lane l: bytes [base + 4l, base + 4l + 4),
+// zero past the end), loaded with one coalesced access.  The frame, block and literals headers and
+// the Huffman jump table are then read with v_readlane instead of a chain of dependent byte loads
+// from HBM.  Bytes outside the window fall back to a global load.
+// ---------------------------------------------------------------------------------------------
+struct HdrWin {
+    uint32_t w;
+    size_t base;
+};
+__device__ __forceinline__ void hw_load(HdrWin& h, const uint8_t* src, size_t srcSize, size_t base)
+{
+    const size_t i = base + 4u * (size_t)lane_id();
+    uint32_t v = 0;
+    if (i + 4 <= srcSize) {
+        v = ld32u(src + i);
+    } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) v |= (i + b < srcSize) ? (uint32_t)gb(src + i + b) << (8 * b) : 0u;
+    }
+    h.w = v;
+    h.base = base;
+}
+// byte at pos (wave-uniform); pos must be < the frame size the window was loaded with
+__device__ __forceinline__ uint32_t hw_byte(const HdrWin& h, const uint8_t* src, size_t pos)
+{
+    const size_t d = pos - h.base;
+    if (pos >= h.base && d < 256) return (readlane_u32(h.w, (int)(d >> 2)) >> (8 * (d & 3))) & 0xFFu;
+    return gb(src + pos);
+}
+// little-endian 16/24/32-bit values at pos (each byte < the frame size)
+__device__ __forceinline__ uint32_t hw_u16(const HdrWin& h, const uint8_t* src, size_t pos)
+{
+    return hw_byte(h, src, pos) | (hw_byte(h, src, pos + 1) << 8);
+}
+__device__ __forceinline__ uint32_t hw_u24(const HdrWin& h, const uint8_t* src, size_t pos)
+{
+    return hw_u16(h, src, pos) | (hw_byte(h, src, pos + 2) << 16);
+}
+__device__ __forceinline__ uint32_t hw_u32(const HdrWin& h, const uint8_t* src, size_t pos)
+{
+    return hw_u16(h, src, pos) | (hw_u16(h, src, pos + 2) << 16);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -235,38 +277,45 @@ __device__ __forceinline__ size_t ncount_lds(int16_t* norm, unsigned* maxSVPtr, 
     return used;
 }
 
-// FSE_buildDTable for the weight alphabet (tableLog <= 6) into sDec.wdt
+// FSE_buildDTable for the weight alphabet (tableLog <= 6, maxSV <= 12) into sDec.wdt, one table
+// entry per lane.  The serial spread visits positions (k * step) & mask, skipping those above
+// highThreshold (the -1 symbols' slots, assigned from the top in symbol order), and gives the k-th
+// valid position to the symbol whose cumulative positive count covers k: lane u computes its
+// position, its rank among the valid ones (ballot + mbcnt) and that symbol directly.  The state
+// of entry u counts the earlier entries of its symbol (one ballot per symbol).
 __device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxSV, unsigned tableLog)
 {
+    const uint32_t lane = (uint32_t)lane_id();
     const uint32_t tableSize = 1u << tableLog;
     const uint32_t mask = tableSize - 1;
     const uint32_t step = (tableSize >> 1) + (tableSize >> 3) + 3;
-    uint32_t highThreshold = tableSize - 1;
-    for (unsigned sy = 0; sy <= maxSV; sy++) {
-        if (norm[sy] == -1) {
-            sDec.wdt[highThreshold--].symbol = (uint8_t)sy;
-            sDec.wnext[sy] = 1;
-        } else {
-            sDec.wnext[sy] = (uint16_t)norm[sy];
-        }
-    }
-    uint32_t position = 0;
-    for (unsigned sy = 0; sy <= maxSV; sy++) {
-        for (int i = 0; i < norm[sy]; i++) {
-            sDec.wdt[position].symbol = (uint8_t)sy;
-            position = (position + step) & mask;
-            while (position > highThreshold) position = (position + step) & mask;
-        }
-    }
-    if (position != 0) return false;
+    const int ns = lane <= maxSV ? norm[lane] : 0;
+    const uint32_t low = ns == -1 ? 1u : 0u, cnt = ns > 0 ? (uint32_t)ns : 0u;
+    const uint32_t lowIncl = wave_incl_sum(low), cntIncl = wave_incl_sum(cnt);
+    const uint32_t nLow = readlane_u32(lowIncl, 63), total = readlane_u32(cntIncl, 63);
+    const uint32_t highThreshold = tableSize - 1 - nLow;
+    if (total != highThreshold + 1) return false;  // the serial spread's final `position != 0`
+    if (low) sDec.wdt[tableSize - lowIncl].symbol = (uint8_t)lane;
+    const uint32_t q = (lane * step) & mask;
+    const bool valid = lane < tableSize && q <= highThreshold;
+    const uint32_t k = mbcnt(ballot(valid));
+    uint32_t sym = 0;  // number of symbols whose cumulative count is <= k
+    for (unsigned sy = 0; sy <= maxSV; sy++) sym += readlane_u32(cntIncl, (int)sy) <= k ? 1u : 0u;
+    if (valid) sDec.wdt[q].symbol = (uint8_t)sym;
     lds_sync();
-    for (uint32_t u = 0; u < tableSize; u++) {
-        const uint8_t sy = sDec.wdt[u].symbol;
-        const uint32_t nextState = sDec.wnext[sy];
-        sDec.wnext[sy] = (uint16_t)(nextState + 1);
-        const uint8_t nb = (uint8_t)(tableLog - z1::highbit32(nextState));
-        sDec.wdt[u].nbBits = nb;
-        sDec.wdt[u].newState = (uint16_t)((nextState << nb) - tableSize);
+    const uint32_t su = lane < tableSize ? sDec.wdt[lane].symbol : 0xFFu;
+    uint32_t rank = 0;
+    for (unsigned sy = 0; sy <= maxSV; sy++) {
+        const uint64_t m = ballot(su == sy);
+        rank = su == sy ? mbcnt(m) : rank;
+    }
+    // symbolNext starts at the normalized count (1 for a -1 symbol)
+    const uint32_t start = (uint32_t)__shfl((int)(low ? 1u : cnt), (int)(su & 63u), 64);
+    if (lane < tableSize) {
+        const uint32_t nextState = start + rank;
+        const uint32_t nb = tableLog - z1::highbit32(nextState);
+        sDec.wdt[lane].nbBits = (uint8_t)nb;
+        sDec.wdt[lane].newState = (uint16_t)((nextState << nb) - tableSize);
     }
     lds_sync();
     return true;
@@ -816,35 +865,37 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     S.htab = uni(S.htab);
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
+    HdrWin hw;
     while (ip < srcSize) {
         if (srcSize - ip < 4) return z1::kDecErrSrcSmall;
-        const uint32_t magic = ld32u(src + ip);
+        hw_load(hw, src, srcSize, ip);
+        const uint32_t magic = hw_u32(hw, src, ip);
         if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) {
             if (srcSize - ip < 8) return z1::kDecErrSrcSmall;
-            uint32_t fs = ld32u(src + ip + 4);
+            uint32_t fs = hw_u32(hw, src, ip + 4);
             if (fs > srcSize - ip - 8) return z1::kDecErrSrcSmall;
             ip += 8 + (size_t)fs;
             continue;
         }
         if (magic != z1::kMagic) return z1::kDecErrHeader;
         if (srcSize - ip < 6) return z1::kDecErrSrcSmall;
-        const uint8_t fhd = gb(src + (ip + 4));
+        const uint8_t fhd = (uint8_t)hw_byte(hw, src, ip + 4);
         const unsigned dictIDFlag = fhd & 3, checksum = (fhd >> 2) & 1, singleSegment = (fhd >> 5) & 1, fcsFlag = fhd >> 6;
         if (fhd & 0x08) return z1::kDecErrHeader;
         size_t hpos = ip + 5 + (singleSegment ? 0 : 1);
         const unsigned didSize = dictIDFlag == 0 ? 0 : (dictIDFlag == 1 ? 1 : (dictIDFlag == 2 ? 2 : 4));
         if (hpos + didSize > srcSize) return z1::kDecErrSrcSmall;
         uint32_t dictID = 0;
-        for (unsigned k = 0; k < didSize; k++) dictID |= (uint32_t)gb(src + (hpos + k)) << (8 * k);
+        for (unsigned k = 0; k < didSize; k++) dictID |= hw_byte(hw, src, hpos + k) << (8 * k);
         hpos += didSize;
         if (dictID != 0) return z1::kDecErrHeader;
         const unsigned fcsSize = (fcsFlag == 0) ? (singleSegment ? 1 : 0) : (1u << fcsFlag);
         if (hpos + fcsSize > srcSize) return z1::kDecErrSrcSmall;
         uint64_t fcs = 0;
-        if (fcsSize == 1) fcs = gb(src + (hpos));
-        else if (fcsSize == 2) fcs = (uint64_t)(gb(src + (hpos)) | (gb(src + (hpos + 1)) << 8)) + 256;
-        else if (fcsSize == 4) fcs = ld32u(src + hpos);
-        else if (fcsSize == 8) fcs = ld64u(src + hpos);
+        if (fcsSize == 1) fcs = hw_byte(hw, src, hpos);
+        else if (fcsSize == 2) fcs = (uint64_t)hw_u16(hw, src, hpos) + 256;
+        else if (fcsSize == 4) fcs = hw_u32(hw, src, hpos);
+        else if (fcsSize == 8) fcs = (uint64_t)hw_u32(hw, src, hpos) | ((uint64_t)hw_u32(hw, src, hpos + 4) << 32);
         hpos += fcsSize;
         ip = hpos;
         const size_t frameStart = op;
@@ -855,7 +906,8 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
         SeqState fs;  // frame state of the sequences stage: repeat offsets, table validity
         while (true) {
             if (srcSize - ip < 3) return z1::kDecErrSrcSmall;
-            const uint32_t bh = (uint32_t)gb(src + (ip)) | ((uint32_t)gb(src + (ip + 1)) << 8) | ((uint32_t)gb(src + (ip + 2)) << 16);
+            if (ip - hw.base + 8 > 256) hw_load(hw, src, srcSize, ip);  // a later block: headers at its start
+            const uint32_t bh = hw_u24(hw, src, ip);
             ip += 3;
             const unsigned last = bh & 1, btype = (bh >> 1) & 3;
             const size_t bsize = bh >> 3;
@@ -863,14 +915,14 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
             if (btype == z1::kBtRaw) {
                 if (bsize > srcSize - ip) return z1::kDecErrSrcSmall;
                 if (op + bsize > dstCap) return z1::kDecErrDstSmall;
-                wave_copy(dst + op, src + ip, bsize);
+                wave_copy8(dst + op, src + ip, bsize);
                 ip += bsize;
                 op += bsize;
                 P.mark(5);
             } else if (btype == z1::kBtRle) {
                 if (ip + 1 > srcSize) return z1::kDecErrSrcSmall;
                 if (op + bsize > dstCap) return z1::kDecErrDstSmall;
-                wave_fill(dst + op, gb(src + (ip)), bsize);
+                wave_fill(dst + op, (uint8_t)hw_byte(hw, src, ip), bsize);
                 ip += 1;
                 op += bsize;
             } else {
@@ -879,26 +931,27 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                 const uint8_t* blk = src + ip;
                 // ---- literals section header
                 if (bsize < 1) return z1::kDecErrCorrupt;
-                const unsigned ltype = gb(blk + (0)) & 3, sf = (gb(blk + (0)) >> 2) & 3;
+                const uint32_t b0 = hw_byte(hw, src, ip);
+                const unsigned ltype = b0 & 3, sf = (b0 >> 2) & 3;
                 size_t lh, rs, cs = 0;
                 bool single = false;
                 if (ltype == z1::kSetBasic || ltype == z1::kSetRle) {
-                    if (sf == 0 || sf == 2) { lh = 1; rs = gb(blk + (0)) >> 3; }
-                    else if (sf == 1) { if (bsize < 2) return z1::kDecErrCorrupt; lh = 2; rs = (gb(blk + (0)) >> 4) + ((size_t)gb(blk + (1)) << 4); }
-                    else { if (bsize < 3) return z1::kDecErrCorrupt; lh = 3; rs = (gb(blk + (0)) >> 4) + ((size_t)gb(blk + (1)) << 4) + ((size_t)gb(blk + (2)) << 12); }
+                    if (sf == 0 || sf == 2) { lh = 1; rs = b0 >> 3; }
+                    else if (sf == 1) { if (bsize < 2) return z1::kDecErrCorrupt; lh = 2; rs = (b0 >> 4) + ((size_t)hw_byte(hw, src, ip + 1) << 4); }
+                    else { if (bsize < 3) return z1::kDecErrCorrupt; lh = 3; rs = (b0 >> 4) + ((size_t)hw_byte(hw, src, ip + 1) << 4) + ((size_t)hw_byte(hw, src, ip + 2) << 12); }
                     cs = (ltype == z1::kSetBasic) ? rs : 1;
                 } else {
                     if (bsize < 5) return z1::kDecErrCorrupt;
-                    const uint32_t lhc = ld32u(blk);
+                    const uint32_t lhc = hw_u32(hw, src, ip);
                     if (sf <= 1) { lh = 3; single = (sf == 0); rs = (lhc >> 4) & 0x3FF; cs = (lhc >> 14) & 0x3FF; }
                     else if (sf == 2) { lh = 4; rs = (lhc >> 4) & 0x3FFF; cs = lhc >> 18; }
-                    else { lh = 5; rs = (lhc >> 4) & 0x3FFFF; cs = (lhc >> 22) + ((size_t)gb(blk + (4)) << 10); }
+                    else { lh = 5; rs = (lhc >> 4) & 0x3FFFF; cs = (lhc >> 22) + ((size_t)hw_byte(hw, src, ip + 4) << 10); }
                 }
                 if (rs > z1::kMaxSrc || lh + cs > bsize) return z1::kDecErrCorrupt;
                 const uint8_t* seqSrc = blk + lh + cs;
                 const size_t seqSize = bsize - lh - cs;
                 if (seqSize < 1) return z1::kDecErrCorrupt;
-                const bool noSeq = (seqSrc[0] == 0);
+                const bool noSeq = (hw_byte(hw, src, ip + lh + cs) == 0);
                 if (noSeq && seqSize != 1) return z1::kDecErrCorrupt;
                 if (noSeq && op + rs > dstCap) return z1::kDecErrDstSmall;
                 uint8_t* litOut = noSeq ? dst + op : S.lit;
@@ -909,7 +962,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     else lit = blk + lh;
                     P.mark(5);
                 } else if (ltype == z1::kSetRle) {
-                    wave_fill(litOut, gb(blk + (lh)), rs);
+                    wave_fill(litOut, (uint8_t)hw_byte(hw, src, ip + lh), rs);
                     P.mark(5);
                 } else {
                     const uint8_t* hp = blk + lh;
@@ -939,7 +992,14 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     } else if (gt) {
                         ok = huf_decode4_serial(hufTl, hp, remain, litOut, (uint32_t)rs, gt);
                     } else {
-                        ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, P);
+                        if (remain < 6) {
+                            ok = false;
+                        } else {
+                            const size_t jp = (size_t)(hp - src);  // the jump table, from the header window
+                            ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs,
+                                                  hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16),
+                                                  hw_u16(hw, src, jp + 4), P);
+                        }
                     }
                     if (ballot(!ok)) return z1::kDecErrHufStream;
                     P.mark(2);

@@ -27,7 +27,8 @@ constexpr unsigned kFseMaxTableLog = 12;
 constexpr unsigned kLLFSELog = 9, kMLFSELog = 9, kOffFSELog = 8;
 constexpr unsigned kMaxLL = 35, kMaxML = 52, kMaxOff = 31, kDefaultMaxOff = 28;
 constexpr unsigned kLLDefaultNormLog = 6, kMLDefaultNormLog = 6, kOFDefaultNormLog = 5;
-constexpr size_t kMaxSrc = 131072;  // one block: the GPU path's per-stream limit
+constexpr size_t kMaxSrc = 131072;        // ZSTD_BLOCKSIZE_MAX: one block (literals, sequences per block)
+constexpr size_t kMaxFrameSrc = 524288;  // largest stream encoded here: a single-segment frame (windowLog 19)
 
 enum : unsigned { kSetBasic = 0, kSetRle = 1, kSetCompressed = 2, kSetRepeat = 3 };
 enum : unsigned { kBtRaw = 0, kBtRle = 1, kBtCompressed = 2 };
@@ -108,7 +109,8 @@ PGN_HD unsigned ml_code(uint32_t mlBase)
 // ---------------------------------------------------------------------------------------------
 // Level-1 compression parameters: row `level 1` of the four srcSize tiers of
 // ZSTD_defaultCParameters, then ZSTD_adjustCParams_internal (window shrunk to the source,
-// hashLog <= windowLog + 1, windowLog >= 10).
+// hashLog <= windowLog + 1, windowLog >= 10); equal to libzstd 1.4.8/1.4.9's
+// ZSTD_getCParams(1, srcSize, 0) for every size up to kMaxFrameSrc (tests/test_zstd_model.py).
 // ---------------------------------------------------------------------------------------------
 struct Params {
     unsigned windowLog, hashLog, mls;
@@ -117,7 +119,9 @@ PGN_HD Params level1_params(size_t srcSize)
 {
     Params p;
     if (srcSize <= 16384) { p.windowLog = 14; p.hashLog = 15; p.mls = 5; }
-    else { p.windowLog = 17; p.hashLog = 13; p.mls = 6; }  // srcSize <= 128 KiB tier
+    else if (srcSize <= 131072) { p.windowLog = 17; p.hashLog = 13; p.mls = 6; }
+    else if (srcSize <= 262144) { p.windowLog = 18; p.hashLog = 14; p.mls = 6; }
+    else { p.windowLog = 19; p.hashLog = 14; p.mls = 7; }
     unsigned srcLog = (srcSize < 64) ? 6u : highbit32((uint32_t)(srcSize - 1)) + 1u;
     if (p.windowLog > srcLog) p.windowLog = srcLog;
     if (p.hashLog > p.windowLog + 1) p.hashLog = p.windowLog + 1;
@@ -142,13 +146,14 @@ PGN_HD void wr16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v
 PGN_HD void wr24(uint8_t* p, uint32_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); }
 PGN_HD void wr32(uint8_t* p, uint32_t v) { wr16(p, v); wr16(p + 2, v >> 16); }
 
-// ZSTD_hashPtr for mls 5 / 6 on 8 readable bytes.
-PGN_HD uint32_t hash_at(const uint8_t* p, unsigned hlog, unsigned mls)
+// ZSTD_hashPtr for mls 5 / 6 / 7 of the 8-byte little-endian word at a position.
+PGN_HD uint32_t hash_word(uint64_t v, unsigned hlog, unsigned mls)
 {
-    uint64_t v = rd64(p);
     if (mls == 5) return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - hlog));
-    return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - hlog));
+    if (mls == 6) return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - hlog));
+    return (uint32_t)(((v << 8) * 58295818150454627ull) >> (64 - hlog));
 }
+PGN_HD uint32_t hash_at(const uint8_t* p, unsigned hlog, unsigned mls) { return hash_word(rd64(p), hlog, mls); }
 
 // ---------------------------------------------------------------------------------------------
 // Frame header (ZSTD_writeFrameHeader, single segment, content size present, no checksum/dictID)
@@ -181,9 +186,10 @@ PGN_HD size_t write_rawrle_lit_header(uint8_t* op, size_t n, unsigned type)
     return fl;
 }
 PGN_HD size_t huf_lit_header_size(size_t n) { return 3 + (n >= 1024) + (n >= 16384); }
-PGN_HD void write_huf_lit_header(uint8_t* op, size_t lhSize, size_t srcSize, size_t cLitSize, bool singleStream)
+// hType: kSetCompressed (a new table) or kSetRepeat (the previous block's table, "treeless")
+PGN_HD void write_huf_lit_header(uint8_t* op, size_t lhSize, size_t srcSize, size_t cLitSize, bool singleStream,
+                                 unsigned hType = kSetCompressed)
 {
-    const unsigned hType = kSetCompressed;
     if (lhSize == 3) {
         wr24(op, (uint32_t)(hType + ((!singleStream) << 2) + (srcSize << 4) + (cLitSize << 14)));
     } else if (lhSize == 4) {

@@ -1,5 +1,5 @@
 // zstd1_model.h -- serial composition of zstd1_common.h into a full `ZSTD_compress(.., 1)` for one
-// source of at most 128 KiB (single block), and a spec (RFC 8878) frame decoder.
+// source of at most kMaxFrameSrc (512 KiB: a single-segment frame of up to four 128 KiB blocks).
 //
 // Host and device: the GPU kernels run the serial parts of these on one lane; the host build
 // (libpgn_model.so, test-only) lets the test-suite fuzz the exact same code against libzstd.
@@ -10,12 +10,14 @@ namespace pgn {
 namespace z1 {
 
 // ---------------------------------------------------------------------------------------------
-// ZSTD_compressBlock_fast (libzstd 1.4.x, two positions per step, kSearchStrength 8, stepSize 2),
-// fresh context: window base = src - 1 (prefixStartIndex 1), hash table zeroed, reps {1, 4, 8}
-// with offset_2 invalidated at the first position.  Positions below are offsets into src; table
-// entries hold indices (= offset + 1).  Appends sequences; literals are implied by the sequences
-// (the literal bytes are src[anchor .. anchor+litLength)).  Returns nbSeq; *lastLL = trailing
-// literal run.
+// ZSTD_compressBlock_fast (libzstd 1.4.x, two positions per step, kSearchStrength 8, stepSize 2) over
+// the block [start, end) of a source whose window is the whole source (single segment): window base
+// = src - 1 (prefixStartIndex 1), table entries hold indices (= offset + 1) and persist across the
+// blocks of a frame (the caller zeroes the table once per frame).  rep[0..1] are the confirmed
+// repeat offsets on entry and the block's candidates on exit (ZSTD_compressBlock_fast_generic's
+// offsetSaved rule); at the first position of the frame, offset_2 (4) > maxRep (1) is invalidated.
+// Appends sequences (literal runs are implied: src[anchor .. anchor + litLength)); returns nbSeq,
+// *lastLL = trailing literal run of the block.
 // ---------------------------------------------------------------------------------------------
 PGN_HD size_t match_count(const uint8_t* src, size_t a, size_t b, size_t end)
 {
@@ -24,15 +26,20 @@ PGN_HD size_t match_count(const uint8_t* src, size_t a, size_t b, size_t end)
     return n;
 }
 
-PGN_HD size_t fast_search_serial(const uint8_t* src, size_t n, const Params& p, uint32_t* ht, Seq* seqs,
-                                 size_t* lastLL)
+PGN_HD size_t fast_search_serial(const uint8_t* src, size_t start, size_t end, const Params& p, uint32_t* ht,
+                                 uint32_t rep[3], Seq* seqs, size_t* lastLL)
 {
     const unsigned hlog = p.hashLog, mls = p.mls;
-    for (size_t i = 0; i < ((size_t)1 << hlog); i++) ht[i] = 0;
     size_t nbSeq = 0;
-    long ip0 = 1, ip1 = 2, anchor = 0;
-    const long iend = (long)n, ilimit = (long)n - 8;
-    uint32_t offset_1 = 1, offset_2 = 0;  // offset_2 (4) > maxRep (1): invalidated
+    long ip0 = (long)start + (start == 0 ? 1 : 0), anchor = (long)start;
+    long ip1 = ip0 + 1;
+    const long iend = (long)end, ilimit = (long)end - 8;
+    uint32_t offset_1 = rep[0], offset_2 = rep[1], offsetSaved = 0;
+    {
+        const uint32_t maxRep = (uint32_t)ip0;  // current - windowLow = (ip0 + 1) - 1
+        if (offset_2 > maxRep) { offsetSaved = offset_2; offset_2 = 0; }
+        if (offset_1 > maxRep) { offsetSaved = offset_1; offset_1 = 0; }
+    }
     while (ip1 < ilimit) {
         long ip2 = ip0 + 2;
         uint32_t h0 = hash_at(src + ip0, hlog, mls);
@@ -103,14 +110,25 @@ PGN_HD size_t fast_search_serial(const uint8_t* src, size_t n, const Params& p, 
         }
         ip1 = ip0 + 1;
     }
+    rep[0] = offset_1 ? offset_1 : offsetSaved;
+    rep[1] = offset_2 ? offset_2 : offsetSaved;
     *lastLL = (size_t)(iend - anchor);
     return nbSeq;
 }
 
 // ---------------------------------------------------------------------------------------------
-// Literals section (ZSTD_compressLiterals -> HUF_compress{1,4}X_repeat with a fresh table).
-// `work` must hold a LitWork.  Returns section size written at dst.
+// Literals section (ZSTD_compressLiterals -> HUF_compress{1,4}X_repeat).  `prev` is the Huffman
+// table state the frame carries from its last compressed block (HUF_repeat_none on the first
+// block; HUF_repeat_check once a table was built -- level 1 never reaches HUF_repeat_valid);
+// `next` receives this block's state (confirmed by the caller only if the block is emitted
+// compressed).  `work` must hold a LitWork.  Returns the section size written at dst.
 // ---------------------------------------------------------------------------------------------
+struct HufState {
+    uint8_t nbBits[256];  // 0 for symbols the table does not hold
+    uint16_t val[256];
+    bool check;           // HUF_repeat_check: the table may be reused
+};
+
 struct LitWork {
     uint32_t count[256];
     HufNode nodes[2 * 256 + 1];
@@ -136,12 +154,40 @@ PGN_HD size_t huf_encode_1x(uint8_t* dst, const uint8_t* src, size_t n, const ui
     return bw_close(bw, dst);
 }
 
-PGN_HD size_t compress_literals(uint8_t* dst, const uint8_t* lit, size_t n, LitWork& w)
+// HUF_compress{1,4}X_usingCTable: the streams (and the 4X jump table) at dst; returns their size
+PGN_HD size_t huf_encode_streams(uint8_t* dst, const uint8_t* lit, size_t n, bool singleStream, const uint8_t* nbBits,
+                                 const uint16_t* val)
 {
+    if (singleStream) return huf_encode_1x(dst, lit, n, nbBits, val);
+    const size_t seg = (n + 3) / 4;
+    uint8_t* jt = dst;
+    uint8_t* sp = jt + 6;
+    for (int k = 0; k < 4; k++) {
+        size_t a = seg * (size_t)k, b = (k == 3) ? n : seg * (size_t)(k + 1);
+        size_t c = huf_encode_1x(sp, lit + a, b - a, nbBits, val);
+        if (k < 3) wr16(jt + 2 * k, (uint32_t)c);
+        sp += c;
+    }
+    return (size_t)(sp - dst);
+}
+
+// HUF_estimateCompressedSize
+PGN_HD size_t huf_estimate(const uint8_t* nbBits, const uint32_t* count, unsigned maxSym)
+{
+    size_t bits = 0;
+    for (unsigned s = 0; s <= maxSym; s++) bits += (size_t)nbBits[s] * count[s];
+    return bits >> 3;
+}
+
+PGN_HD size_t compress_literals(uint8_t* dst, const uint8_t* lit, size_t n, LitWork& w, const HufState& prev,
+                                HufState& next)
+{
+    next = prev;  // "Prepare nextEntropy assuming reusing the existing table"
     if (n <= 63) return write_raw_literals(dst, lit, n);
     const size_t minGain = (n >> 6) + 2;
     const size_t lhSize = huf_lit_header_size(n);
     const bool singleStream = n < 256;
+    const bool preferRepeat = n <= 1024;  // strategy < ZSTD_lazy
     // HIST_count_wksp
     for (int s = 0; s < 256; s++) w.count[s] = 0;
     for (size_t i = 0; i < n; i++) w.count[lit[i]]++;
@@ -155,33 +201,42 @@ PGN_HD size_t compress_literals(uint8_t* dst, const uint8_t* lit, size_t n, LitW
         return fl + 1;
     }
     if (largest <= (n >> 7) + 4) return write_raw_literals(dst, lit, n);
-    unsigned huffLog = huf_optimal_table_log(kHufTableLogDefault, n, maxSym);
-    for (int i = 0; i < 2 * 256 + 1; i++) { w.nodes[i].count = 0; w.nodes[i].parent = 0; w.nodes[i].byte = 0; w.nodes[i].nbBits = 0; }
-    huf_sort_serial(w.nodes + 1, w.count, maxSym);
-    huffLog = huf_build_from_sorted(w.nodes, maxSym, huffLog, w.nbBits, w.val);
+    // HUF_validateCTable: the previous table must code every symbol present
+    bool repeat = prev.check;
+    if (repeat)
+        for (unsigned s = 0; s <= maxSym; s++) repeat = repeat && !(w.count[s] != 0 && prev.nbBits[s] == 0);
     uint8_t* op = dst + lhSize;
-    size_t hSize = huf_write_ctable(op, w.nbBits, maxSym, huffLog, w.fct, w.scratch);
-    if (hSize == 0) return write_raw_literals(dst, lit, n);   // HUF error -> raw
-    if (hSize + 12 >= n) return write_raw_literals(dst, lit, n);
-    size_t cSize;
-    if (singleStream) {
-        cSize = huf_encode_1x(op + hSize, lit, n, w.nbBits, w.val);
-    } else {
-        const size_t seg = (n + 3) / 4;
-        uint8_t* jt = op + hSize;
-        uint8_t* sp = jt + 6;
-        for (int k = 0; k < 4; k++) {
-            size_t a = seg * (size_t)k, b = (k == 3) ? n : seg * (size_t)(k + 1);
-            size_t c = huf_encode_1x(sp, lit + a, b - a, w.nbBits, w.val);
-            if (k < 3) wr16(jt + 2 * k, (uint32_t)c);
-            sp += c;
+    bool useOld = repeat && preferRepeat;
+    size_t hSize = 0;
+    if (!useOld) {
+        unsigned huffLog = huf_optimal_table_log(kHufTableLogDefault, n, maxSym);
+        for (int i = 0; i < 2 * 256 + 1; i++) { w.nodes[i].count = 0; w.nodes[i].parent = 0; w.nodes[i].byte = 0; w.nodes[i].nbBits = 0; }
+        huf_sort_serial(w.nodes + 1, w.count, maxSym);
+        huffLog = huf_build_from_sorted(w.nodes, maxSym, huffLog, w.nbBits, w.val);
+        for (unsigned s = maxSym + 1; s < 256; s++) { w.nbBits[s] = 0; w.val[s] = 0; }
+        hSize = huf_write_ctable(op, w.nbBits, maxSym, huffLog, w.fct, w.scratch);
+        if (hSize == 0) return write_raw_literals(dst, lit, n);  // HUF_writeCTable error -> raw
+        if (repeat) {  // is the previous table still the better one?
+            const size_t oldSize = huf_estimate(prev.nbBits, w.count, maxSym);
+            const size_t newSize = huf_estimate(w.nbBits, w.count, maxSym);
+            if (oldSize <= hSize + newSize || hSize + 12 >= n) useOld = true;
         }
-        cSize = (size_t)(sp - (op + hSize));
+        if (!useOld && hSize + 12 >= n) return write_raw_literals(dst, lit, n);
     }
-    size_t total = hSize + cSize;
+    size_t total;
+    if (useOld) {  // HUF_compressCTable_internal with the previous table: no description
+        const size_t c = huf_encode_streams(op, lit, n, singleStream, prev.nbBits, prev.val);
+        if (c >= n - 1 || c >= n - minGain) return write_raw_literals(dst, lit, n);
+        write_huf_lit_header(dst, lhSize, n, c, singleStream, kSetRepeat);
+        return lhSize + c;
+    }
+    const size_t c = huf_encode_streams(op + hSize, lit, n, singleStream, w.nbBits, w.val);
+    total = hSize + c;
     if (total >= n - 1) return write_raw_literals(dst, lit, n);        // HUF_compressCTable_internal
     if (total >= n - minGain) return write_raw_literals(dst, lit, n);  // ZSTD_compressLiterals
     write_huf_lit_header(dst, lhSize, n, total, singleStream);
+    for (int s = 0; s < 256; s++) { next.nbBits[s] = w.nbBits[s]; next.val[s] = w.val[s]; }
+    next.check = true;  // a newly built table: HUF_repeat_check
     return lhSize + total;
 }
 
@@ -299,7 +354,7 @@ PGN_HD size_t compress_sequences(uint8_t* dst, const Seq* seqs, size_t nbSeq, ui
 }
 
 // ---------------------------------------------------------------------------------------------
-// Block + frame around pre-computed sections.
+// Blocks + frame (ZSTD_compress_frameChunk / ZSTD_compressBlock_internal, libzstd 1.4.8/1.4.9).
 // ---------------------------------------------------------------------------------------------
 PGN_HD size_t write_empty_frame(uint8_t* dst)
 {
@@ -318,42 +373,90 @@ PGN_HD size_t write_raw_block_frame(uint8_t* dst, const uint8_t* src, size_t n)
 struct CompressWork {
     LitWork lit;
     SeqWork seq;
+    HufState huf[2];  // confirmed (previous compressed block) and candidate (this block)
 };
 
-// Full serial ZSTD_compress(dst, bound, src, n, 1) for n <= kMaxSrc.  `ht`: 2^15 entries;
-// `seqs`, `llC/ofC/mlC`: n/4 + 1 entries; `litbuf`: n bytes.  dst capacity >= compress_bound(n).
+// ZSTD_isRLE
+PGN_HD bool block_is_rle(const uint8_t* p, size_t n)
+{
+    for (size_t i = 1; i < n; i++)
+        if (p[i] != p[0]) return false;
+    return true;
+}
+
+// One block [start, start + bs) of a frame: its header and body at dst; returns bytes written.
+// `rep` / `huf` are the frame's confirmed state, updated when the block is emitted compressed
+// (ZSTD_confirmRepcodesAndEntropyTables).  Sequence FSE tables never repeat at level 1 (the
+// repeat mode stays "check", never "valid"), so they carry no state.
+PGN_HD size_t compress_block(uint8_t* dst, const uint8_t* src, size_t start, size_t bs, bool last, bool first,
+                             const Params& p, uint32_t* ht, uint32_t rep[3], Seq* seqs, uint8_t* llC, uint8_t* ofC,
+                             uint8_t* mlC, uint8_t* litbuf, CompressWork& w)
+{
+    const uint8_t* blk = src + start;
+    size_t cSize = 0;  // 0: raw block, 1: RLE block, else compressed body size
+    if (bs >= 7) {     // MIN_CBLOCK_SIZE + ZSTD_blockHeaderSize + 1: below it no compression is tried
+        uint32_t nrep[3] = {rep[0], rep[1], rep[2]};
+        size_t lastLL = 0;
+        const size_t nbSeq = fast_search_serial(src, start, start + bs, p, ht, nrep, seqs, &lastLL);
+        const uint8_t* lit = blk;
+        size_t nLit = bs;
+        if (nbSeq > 0) {
+            size_t pos = start, o = 0;
+            for (size_t i = 0; i < nbSeq; i++) {
+                for (uint32_t k = 0; k < seqs[i].litLength; k++) litbuf[o++] = src[pos + k];
+                pos += seqs[i].litLength + seqs[i].mlBase + 3;
+            }
+            for (size_t k = 0; k < lastLL; k++) litbuf[o++] = src[pos + k];
+            lit = litbuf;
+            nLit = o;
+        }
+        uint8_t* body = dst + 3;
+        const size_t litSize = compress_literals(body, lit, nLit, w.lit, w.huf[0], w.huf[1]);
+        const size_t seqSize = compress_sequences(body + litSize, seqs, nbSeq, llC, ofC, mlC, w.seq);
+        const size_t maxCSize = bs - ((bs >> 6) + 2);
+        if (seqSize != (size_t)-1 && seqSize != (size_t)-2 && litSize + seqSize < maxCSize) cSize = litSize + seqSize;
+        // a later block of one repeated byte is an RLE block (never the first: decoders <= 1.4.3)
+        if (!first && cSize < 25 && block_is_rle(blk, bs)) cSize = 1;
+        if (cSize > 1) {  // ZSTD_confirmRepcodesAndEntropyTables
+            rep[0] = nrep[0];
+            rep[1] = nrep[1];
+            rep[2] = nrep[2];
+            w.huf[0] = w.huf[1];
+        }
+    }
+    if (cSize == 0) {
+        wr24(dst, (uint32_t)((last ? 1u : 0u) + (kBtRaw << 1) + (bs << 3)));
+        for (size_t i = 0; i < bs; i++) dst[3 + i] = blk[i];
+        return 3 + bs;
+    }
+    if (cSize == 1) {
+        wr24(dst, (uint32_t)((last ? 1u : 0u) + (kBtRle << 1) + (bs << 3)));
+        dst[3] = blk[0];
+        return 4;
+    }
+    wr24(dst, (uint32_t)((last ? 1u : 0u) + (kBtCompressed << 1) + (cSize << 3)));
+    return 3 + cSize;
+}
+
+// Full serial ZSTD_compress(dst, bound, src, n, 1) for n <= kMaxFrameSrc (blocks of 128 KiB).
+// `ht`: 2^15 entries; `seqs`, `llC/ofC/mlC`: kMaxSrc/4 + 2 entries; `litbuf`: kMaxSrc bytes
+// (per block); dst capacity >= compress_bound(n).
 PGN_HD size_t compress_serial(uint8_t* dst, const uint8_t* src, size_t n, uint32_t* ht, Seq* seqs, uint8_t* llC,
                               uint8_t* ofC, uint8_t* mlC, uint8_t* litbuf, CompressWork& w)
 {
     if (n == 0) return write_empty_frame(dst);
     if (n < 7) return write_raw_block_frame(dst, src, n);
-    Params p = level1_params(n);
-    size_t lastLL = 0;
-    size_t nbSeq = fast_search_serial(src, n, p, ht, seqs, &lastLL);
-    // gather literals
-    const uint8_t* lit = src;
-    size_t nLit = n;
-    if (nbSeq > 0) {
-        size_t pos = 0, o = 0;
-        for (size_t i = 0; i < nbSeq; i++) {
-            for (uint32_t k = 0; k < seqs[i].litLength; k++) litbuf[o++] = src[pos + k];
-            pos += seqs[i].litLength + seqs[i].mlBase + 3;
-        }
-        for (size_t k = 0; k < lastLL; k++) litbuf[o++] = src[pos + k];
-        lit = litbuf;
-        nLit = o;
+    const Params p = level1_params(n);
+    for (size_t i = 0; i < ((size_t)1 << p.hashLog); i++) ht[i] = 0;
+    uint32_t rep[3] = {1, 4, 8};
+    w.huf[0].check = false;
+    for (int s = 0; s < 256; s++) { w.huf[0].nbBits[s] = 0; w.huf[0].val[s] = 0; }
+    size_t o = write_frame_header(dst, n);
+    for (size_t start = 0; start < n; start += kMaxSrc) {
+        const size_t bs = (n - start < kMaxSrc) ? n - start : kMaxSrc;
+        o += compress_block(dst + o, src, start, bs, start + bs == n, start == 0, p, ht, rep, seqs, llC, ofC, mlC, litbuf, w);
     }
-    size_t h = frame_header_size(n);
-    uint8_t* body = dst + h + 3;
-    size_t litSize = compress_literals(body, lit, nLit, w.lit);
-    size_t seqSize = compress_sequences(body + litSize, seqs, nbSeq, llC, ofC, mlC, w.seq);
-    size_t maxCSize = n - ((n >> 6) + 2);
-    if (seqSize == (size_t)-1 || seqSize == (size_t)-2 || litSize + seqSize >= maxCSize)
-        return write_raw_block_frame(dst, src, n);
-    size_t cSize = litSize + seqSize;
-    write_frame_header(dst, n);
-    wr24(dst + h, (uint32_t)(1u + (kBtCompressed << 1) + (cSize << 3)));
-    return h + 3 + cSize;
+    return o;
 }
 
 }  // namespace z1

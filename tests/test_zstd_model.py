@@ -113,3 +113,66 @@ def test_decoder_other_encoder_settings(level, wlog):
         fr = O.zstd_compress_ex(b, level, wlog)
         r, out = model_decompress(fr, n)
         assert r == n and out == b.tobytes(), (level, wlog, n, kind, r)
+
+
+# ---- multi-block frames (sources above one 128 KiB block, up to 512 KiB) -----------------------
+MB_SIZES = [131073, 131078, 131079, 131200, 200000, 262144, 262145, 300000, 393216, 524288]
+
+
+def gen_multiblock(rng, n, kind):
+    """Cross-block shapes: later blocks that repeat earlier data (matches into the previous block),
+    a block of one byte (RLE block), blocks whose literals fit / do not fit the previous Huffman
+    table (table repeat vs a new table), a short last block, few literals in a later block (the
+    preferRepeat path)."""
+    B = 131072
+    if kind < 7:
+        return gen(rng, n, kind)
+    b = np.resize(gen(rng, n, int(rng.integers(1, 6))), n).astype(np.uint8)
+    if kind == 7:  # later blocks copy earlier ones with light edits
+        for s in range(B, n, B):
+            L = min(B, n - s)
+            b[s:s + L] = b[s - B:s - B + L]
+            idx = rng.integers(s, s + L, max(1, L // 500))
+            b[idx] = rng.integers(0, 256, idx.size)
+    elif kind == 8:  # one block of a single repeated byte
+        s = B * int(rng.integers(1, (n - 1) // B + 1))
+        b[s:min(n, s + B)] = int(rng.integers(0, 256))
+    elif kind == 9:  # second block: a subset of the first block's symbols, other proportions
+        k = int(rng.integers(2, 40))
+        b[:B] = rng.integers(0, 64, B)
+        b[B:] = rng.choice(k, n - B).astype(np.uint8) * (64 // k if k < 64 else 1)
+    elif kind == 10:  # a later block made of repeats with few literals (<= 1024)
+        for s in range(B, n, B):
+            L = min(B, n - s)
+            b[s:s + L] = np.resize(b[s - 300:s - 300 + 257], L)
+            idx = rng.integers(s, s + L, int(rng.integers(1, 200)))
+            b[idx] = rng.integers(0, 256, idx.size)
+    elif kind == 11:  # a new symbol in a later block invalidates the previous table
+        b[:B] = rng.choice(16, B).astype(np.uint8)
+        b[B:] = rng.choice(16, n - B).astype(np.uint8)
+        b[B + int(rng.integers(0, min(1000, n - B)))] = 200
+    return b
+
+
+@pytest.mark.parametrize("n", MB_SIZES)
+def test_multiblock_sizes(n):
+    rng = np.random.default_rng(n + 7)
+    for kind in range(12):
+        b = np.ascontiguousarray(gen_multiblock(rng, n, kind), dtype=np.uint8)
+        ref = O.zstd_compress1(b)
+        assert model_compress(b) == ref, (n, kind)
+        r, d = model_decompress(ref, b.size)
+        assert r == b.size and d == b.tobytes(), (n, kind)
+
+
+def test_multiblock_fuzz_bounded():
+    rng = np.random.default_rng(777)
+    t0, cnt = time.time(), 0
+    while time.time() - t0 < 20:
+        n = int(rng.integers(131073, 524289))
+        kind = int(rng.integers(0, 12))
+        b = np.ascontiguousarray(gen_multiblock(rng, n, kind), dtype=np.uint8)
+        ref = O.zstd_compress1(b)
+        assert model_compress(b) == ref, (n, kind, cnt)
+        cnt += 1
+    assert cnt > 20
