@@ -30,15 +30,18 @@ typedef enum pgn_status {
     PGN_ERR_REMAINING = 4,        /* "Remaining data at end of signal buffer"       C5.hpp:675-677 */
     PGN_ERR_ZSTD_COMPRESS = 5,    /* "Failed to compress ..."                        C5.hpp:340-342 */
     PGN_ERR_CORRUPT = 6,          /* input on which the reference reads out of bounds (UB there) */
-    PGN_ERR_UNSUPPORTED = 9,      /* chunk larger than PGN_MAX_CHUNK_SAMPLES */
+    PGN_ERR_UNSUPPORTED = 9,      /* chunk larger than PGN_MAX_CHUNK_SAMPLES, or a stream above 512 KiB */
     PGN_ERR_INVALID_ARG = 10,
     PGN_ERR_HIP = 11,             /* HIP runtime failure (message in pgn_last_error) */
     PGN_ERR_NO_DEVICE = 12
 } pgn_status;
 
-/* Largest chunk the GPU path encodes (one zstd block per stream).  The reference writer's default
- * chunk is 102,400 samples (pod5/c++/pod5_format/file_writer.h:22). */
-#define PGN_MAX_CHUNK_SAMPLES 131072u
+/* Largest chunk the GPU path encodes and decodes.  Every stream is one zstd frame of up to four
+ * 128 KiB blocks (ZSTD_compress level 1 as libzstd 1.4.x writes it for sources up to 512 KiB); a VBZ
+ * or C1 svb16 buffer above 512 KiB (noisy chunks near this limit) is PGN_ERR_UNSUPPORTED.  The
+ * reference writer's default chunk is 102,400 samples (pod5/c++/pod5_format/file_writer.h:22) and
+ * the chunk size is a writer option (c_api.h:526-539). */
+#define PGN_MAX_CHUNK_SAMPLES 262144u
 
 /* Per-chunk statistics, the reference's global byte counters (src/c++/copy.cpp:64-85, updated at
  * C5.hpp:318-324,467-471): raw stream sizes then frame sizes, order keys, S, M, Llow, Lhigh. */
@@ -110,7 +113,7 @@ size_t pgn_vbz_compressed_signal_max_size(size_t sample_count);
 
 /* pod5::compress_signal(samples, pool, destination) (signal_compression.cpp:21-50): the compressed
  * size in *out_size; a frame larger than dst_capacity is PGN_ERR_ZSTD_COMPRESS ("Failed to compress
- * data").  Chunks whose svb16 buffer exceeds one zstd block (128 KiB) return PGN_ERR_UNSUPPORTED. */
+ * data").  Chunks whose svb16 buffer exceeds 512 KiB return PGN_ERR_UNSUPPORTED. */
 int pgn_vbz_compress_signal(pgn_ctx *ctx, const int16_t *samples, size_t sample_count, uint8_t *dst,
                             size_t dst_capacity, size_t *out_size);
 
@@ -141,7 +144,7 @@ int pgn_vbz_decompress_batch_device(pgn_ctx *ctx, size_t nchunks, const uint8_t 
  * VBZ0 compresses straight into the destination ("Failed to compress data" = PGN_ERR_ZSTD_COMPRESS
  * when the frame does not fit); C1/C2/C3 copy into it unchecked in the reference, here a
  * too-small destination is PGN_ERR_DST_TOO_SMALL with the required size, as for C5/C4.  Streams
- * above one zstd block (128 KiB) return PGN_ERR_UNSUPPORTED. */
+ * above 512 KiB return PGN_ERR_UNSUPPORTED. */
 typedef enum pgn_variant {
     PGN_VARIANT_C5 = 0,
     PGN_VARIANT_C4 = 1,

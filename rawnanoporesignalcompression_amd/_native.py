@@ -26,7 +26,7 @@ PGN_ERR_INVALID_ARG = 10
 PGN_ERR_HIP = 11
 PGN_ERR_NO_DEVICE = 12
 
-PGN_MAX_CHUNK_SAMPLES = 131072
+PGN_MAX_CHUNK_SAMPLES = 262144
 # pgn_variant: the reference's compile-time COMPRESSOR_* variants (pgnano.cpp:70-92)
 VARIANTS = {"C5": 0, "C4": 1, "C1": 2, "C2": 3, "C3": 4, "VBZ0": 5}
 PGN_STATS_PER_CHUNK = 10

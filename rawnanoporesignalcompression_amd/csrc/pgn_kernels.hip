@@ -22,8 +22,10 @@ namespace pgn {
 
 constexpr uint32_t kMaxSamples = PGN_MAX_CHUNK_SAMPLES;
 constexpr uint32_t kMaxStream = kMaxSamples;            // largest C5 stream (M/Llow/Lhigh <= n)
-constexpr uint32_t kMaxEncSeq = kMaxStream / 4 + 2;      // every match covers >= 4 bytes
-constexpr uint32_t kMaxDecSeq = kMaxStream / 3 + 2;      // any valid block: matches >= 3 bytes
+// literals and sequences live per zstd block (<= 128 KiB); a frame's blocks reuse them
+constexpr uint32_t kMaxEncSeq = (uint32_t)z1::kMaxSrc / 4 + 2;  // every match covers >= 4 bytes
+constexpr uint32_t kMaxDecSeq = (uint32_t)z1::kMaxSrc / 3 + 2;  // any valid block: matches >= 3 bytes
+static_assert(kMaxStream <= z1::kMaxFrameSrc, "a C5 stream must fit one encoder frame");
 constexpr int kStreams = 5;
 // Codecs of a batch call: the pgnano C5 variant (5 zstd frames per chunk) and the pod5 VBZ codec
 // (one zstd frame per chunk).  Both share the per-chunk buffers and the zstd kernels.
@@ -63,7 +65,7 @@ constexpr size_t kChunkFrameBytes = frame_off(kStreams);
 // Scratch of one resident zstd-encode workgroup ("slot")
 // ---------------------------------------------------------------------------------------------
 struct EncLayout {
-    size_t ht, lit, seqs, codes, seqSection, seqWork, bytes;
+    size_t ht, lit, seqs, codes, seqSection, seqWork, huf, bytes;
 };
 __host__ __device__ inline EncLayout enc_layout()
 {
@@ -71,11 +73,12 @@ __host__ __device__ inline EncLayout enc_layout()
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o = align_up(o + n + 64, 256); return r; };
     l.ht = take((size_t)4 << 15);
-    l.lit = take(kMaxStream);
+    l.lit = take(z1::kMaxSrc);
     l.seqs = take(sizeof(z1::Seq) * kMaxEncSeq);
     l.codes = take(3 * (size_t)kMaxEncSeq);
     l.seqSection = take(16 + 10 * (size_t)kMaxEncSeq + 1024);
     l.seqWork = take(sizeof(z1::SeqWork));
+    l.huf = take(2 * 256 * 4);
     l.bytes = o;
     return l;
 }
@@ -88,7 +91,7 @@ __host__ __device__ inline DecLayout dec_layout()
     DecLayout l{};
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o = align_up(o + n + 64, 256); return r; };
-    l.lit = take(kMaxStream);
+    l.lit = take(z1::kMaxSrc);
     l.seqs = take(12 * (size_t)kMaxDecSeq);
     l.tables = take(4 * ((size_t)kSeqTab + 4));
     l.htab = take(2u << z1::kHufTableLogMax);
@@ -173,6 +176,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
     S.seqSection = sbase + lay.seqSection;
     S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
     S.maxSeq = kMaxEncSeq;
+    S.huf = (uint32_t*)(sbase + lay.huf);
     uint32_t epoch = a.epochs[blockIdx.x];
     PhaseProf P;
     P.init(a.prof);
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
         if (a.base + g >= a.nchunks) continue;
         const uint32_t n = a.sizes[g * kStreams + s];
         if (a.sizes[g * kStreams] == ~0u) continue;  // unsupported chunk
-        if (++epoch >= 32768u) {  // tag space exhausted: clear the table once
+        if (++epoch >= kTagEpochs) {  // tag space exhausted: clear the table once
             for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
             epoch = 1;
             wave_sync();
@@ -408,7 +412,7 @@ __global__ __launch_bounds__(64) void vbz_split_kernel(EncArgs a)
     const uint32_t pad = (16u - (svb_key_length(n) & 15u)) & 15u;
     const uint32_t m = vbz_split_wave(a.samples + a.sampleOffsets[c], n, a.streams + g * kChunkStreamBytes + pad, W);
     if (lane_id() == 0) {
-        if (m > z1::kMaxSrc) {  // more than one zstd block: not on the GPU path yet
+        if (m > z1::kMaxFrameSrc) {  // larger than one single-segment level-1 frame here
             sz[0] = ~0u;
             a.status[c] = PGN_ERR_UNSUPPORTED;
             a.outSizes[c] = 0;
@@ -528,7 +532,9 @@ __host__ __device__ constexpr int codec_frames(int codec)
 
 // slot scratch of the fused kernels: the zstd scratch, then the chunk's streams (encode: + one
 // frame for a stream that may not fit the destination) or its intermediate (decode)
-__host__ __device__ inline size_t enc_slot_bytes() { return enc_layout().bytes + kChunkStreamBytes + frame_pad(2); }
+// (the frame buffer holds any one stream's frame: a VBZ / C1 svb16 buffer can reach kMaxFrameSrc)
+constexpr size_t kSlotFrameBytes = align_up(frame_bound(z1::kMaxFrameSrc) + 64, 256);
+__host__ __device__ inline size_t enc_slot_bytes() { return enc_layout().bytes + kChunkStreamBytes + kSlotFrameBytes; }
 __host__ __device__ inline size_t dec_slot_bytes() { return dec_layout().bytes + kChunkInterBytes; }
 
 // The split and merge stages as non-inlined calls with wave-uniform arguments: each gets its own
@@ -629,6 +635,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
     S.seqSection = sbase + lay.seqSection;
     S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
     S.maxSeq = kMaxEncSeq;
+    S.huf = (uint32_t*)(sbase + lay.huf);
     uint8_t* streams = sbase + lay.bytes;
     uint8_t* fbuf = streams + kChunkStreamBytes;
     uint32_t epoch = a.epochs[blockIdx.x];
@@ -680,9 +687,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
         }
 #pragma unroll
         for (int s = 0; s < kStreams; s++) sz[s] = uni(sz[s]);
-        bool big = false;  // a stream above one zstd block: not on the GPU encoder
+        bool big = false;  // a stream above one single-segment frame (512 KiB): not on the GPU encoder
 #pragma unroll
-        for (int s = 0; s < nf; s++) big |= sz[s] > z1::kMaxSrc;
+        for (int s = 0; s < nf; s++) big |= sz[s] > z1::kMaxFrameSrc;
         if (big) {
             enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
             continue;
@@ -697,7 +704,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
 #pragma unroll
         for (int s = 0; s < nf; s++) {
             if (s < nf - 1) off += 8;  // length prefixes of all frames but the last (C5.hpp:429-462)
-            if (++epoch >= 32768u) {  // tag space exhausted: clear the table once
+            if (++epoch >= kTagEpochs) {  // tag space exhausted: clear the table once
                 for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
                 epoch = 1;
                 wave_sync();

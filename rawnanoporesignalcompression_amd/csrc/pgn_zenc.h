@@ -87,13 +87,14 @@ __device__ __forceinline__ uint32_t seg_count(const EncLds& L, int k, int s)
 static __shared__ EncLds sEnc;
 
 struct EncScratch {
-    uint32_t* ht;        // 2^15 tagged hash-table entries
+    uint32_t* ht;        // 2^15 tagged hash-table entries (tag << kTagShift | index)
     z1::Seq* seqs;       // <= stream/4 + 2 sequences
     uint8_t* codes;      // 3 * (stream/4 + 2)
     uint8_t* lit;        // gathered literals (stream bytes)
     uint8_t* seqSection; // sequences section staging (compress_bound(stream))
     z1::SeqWork* seqWork;
     uint32_t maxSeq;
+    uint32_t* huf;       // two Huffman tables (code | nbBits << 16, 256 each): confirmed and candidate
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -124,14 +125,17 @@ __device__ inline uint32_t wave_match_count(const uint8_t* src, uint32_t a, uint
     return n;
 }
 
-__device__ inline uint32_t tagged(uint32_t tag, uint32_t idx) { return (tag << 17) | idx; }
+// Hash-table entries: a per-slot epoch tag above a 20-bit index (positions of frames up to
+// kMaxFrameSrc = 512 KiB); the table is cleared once per kTagEpochs streams.
+constexpr uint32_t kTagShift = 20;
+constexpr uint32_t kTagEpochs = 1u << (32 - kTagShift);
+static_assert(z1::kMaxFrameSrc + 2 < (1u << kTagShift), "index field");
+__device__ inline uint32_t tagged(uint32_t tag, uint32_t idx) { return (tag << kTagShift) | idx; }
 
-// ZSTD_hashPtr (mls 5 / 6) over 8 global bytes
+// ZSTD_hashPtr (mls 5 / 6 / 7) over 8 global bytes
 __device__ __forceinline__ uint32_t hash_g(const uint8_t* p, unsigned hlog, unsigned mls)
 {
-    const uint64_t v = ld64u(p);
-    if (mls == 5) return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - hlog));
-    return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - hlog));
+    return z1::hash_word(ld64u(p), hlog, mls);
 }
 
 // Number of equal bytes going backwards from a-1 / b-1, at most `lim` (wave-parallel, 64 per step)
@@ -157,22 +161,33 @@ __device__ inline uint32_t wave_back_count(const uint8_t* src, uint32_t a, uint3
 // table writes (the last writer of a slot wins), the hit is processed as the serial loop does, and
 // the next round starts after it.  Same-slot writers inside a round are found through an LDS filter
 // (one bit per lane per slot), checked exactly only for the lanes whose filter slots collide.
-// Returns nbSeq | lastLiterals << 32.
-__device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ src, uint32_t n, unsigned hlog, unsigned mls,
-                                                  uint32_t* __restrict__ ht, uint32_t tag, z1::Seq* __restrict__ seqs)
+// Searches the block [start, end) of src (table and positions frame-wide, zstd1_model.h
+// fast_search_serial); rep0 / rep1 are the confirmed repeat offsets on entry.
+struct SearchOut {
+    uint32_t nbSeq, lastLL, rep0, rep1;
+};
+__device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ src, uint32_t start, uint32_t end, unsigned hlog,
+                                                   unsigned mls, uint32_t* __restrict__ ht, uint32_t tag,
+                                                   z1::Seq* __restrict__ seqs, uint32_t rep0, uint32_t rep1)
 {
     EncLds& L = sEnc;
     const uint32_t lane = (uint32_t)lane_id();
     src = uni(src);
-    n = uni(n);
+    start = uni(start);
+    end = uni(end);
     hlog = uni(hlog);
     mls = uni(mls);
     ht = uni(ht);
     tag = uni(tag);
     seqs = uni(seqs);
-    const int32_t iend = (int32_t)n, ilimit = (int32_t)n - 8;
-    int32_t ip0 = 1, anchor = 0;
-    uint32_t off1 = 1, off2 = 0;
+    rep0 = uni(rep0);
+    rep1 = uni(rep1);
+    const int32_t iend = (int32_t)end, ilimit = (int32_t)end - 8;
+    int32_t ip0 = (int32_t)start + (start == 0 ? 1 : 0), anchor = (int32_t)start;
+    // ZSTD_compressBlock_fast_generic: repeat offsets beyond the first position are invalidated
+    uint32_t off1 = rep0, off2 = rep1, offSaved = 0;
+    if (off2 > (uint32_t)ip0) { offSaved = off2; off2 = 0; }
+    if (off1 > (uint32_t)ip0) { offSaved = off1; off1 = 0; }
     uint32_t nbSeq = 0;
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
@@ -208,13 +223,8 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
         uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu, t0 = 0, t1 = 0;
         uint64_t M0 = 0, M1 = 0;
         if (valid) {
-            if (mls == 5) {
-                h0 = (uint32_t)(((v8 << 24) * 889523592379ull) >> (64 - hlog));
-                h1 = (uint32_t)((((v8 >> 8) << 24) * 889523592379ull) >> (64 - hlog));
-            } else {
-                h0 = (uint32_t)(((v8 << 16) * 227718039650203ull) >> (64 - hlog));
-                h1 = (uint32_t)((((v8 >> 8) << 16) * 227718039650203ull) >> (64 - hlog));
-            }
+            h0 = z1::hash_word(v8, hlog, mls);
+            h1 = z1::hash_word(v8 >> 8, hlog, mls);
             t0 = gld<uint32_t>(ht + h0);
             t1 = gld<uint32_t>(ht + h1);
             atomicOr((unsigned long long*)&L.filt[h0 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
@@ -241,8 +251,8 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
             L.filt[h1 & (kFiltSlots - 1)] = 0;
         }
         // value each slot holds at my visit: the latest earlier writer in this round, else the table
-        uint32_t m0 = ((t0 >> 17) == tag) ? (t0 & 0x1FFFFu) : 0u;
-        uint32_t m1 = ((t1 >> 17) == tag) ? (t1 & 0x1FFFFu) : 0u;
+        uint32_t m0 = ((t0 >> kTagShift) == tag) ? (t0 & ((1u << kTagShift) - 1u)) : 0u;
+        uint32_t m1 = ((t1 >> kTagShift) == tag) ? (t1 & ((1u << kTagShift) - 1u)) : 0u;
         for (uint64_t cand = M0 & below; cand;) {
             const int jj = 63 - __builtin_clzll(cand);
             const uint32_t pj = L.vpk[jj];
@@ -359,7 +369,12 @@ __device__ __noinline__ uint64_t fast_search_wave(const uint8_t* __restrict__ sr
         }
         wave_sync();
     }
-    return (uint64_t)nbSeq | ((uint64_t)(iend - anchor) << 32);
+    SearchOut r;
+    r.nbSeq = nbSeq;
+    r.lastLL = (uint32_t)(iend - anchor);
+    r.rep0 = off1 ? off1 : offSaved;
+    r.rep1 = off2 ? off2 : offSaved;
+    return r;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1157,20 +1172,33 @@ __device__ inline size_t write_raw_literals_wave(uint8_t* dst, const uint8_t* li
 
 // writeRaw = false: a raw literals section is sized but not written (the caller knows it turns the
 // whole block raw and writes that instead).
-__device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
-                                                PhaseProf& P, uint32_t writeRaw)
+// Huffman table state of the frame (zstd1_model.h compress_literals): prevCw holds the confirmed
+// table of an earlier block (code | nbBits << 16 per symbol) when prevCheck (HUF_repeat_check); a
+// newly built table is written to nextCw when saveNew (a later block may repeat it).
+struct LitOut {
+    uint32_t size;
+    uint32_t newTable;  // a new table was built and used (HUF_repeat_check from here on)
+};
+__device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
+                                                      PhaseProf& P, uint32_t writeRaw, const uint32_t* prevCw,
+                                                      uint32_t prevCheck, uint32_t* nextCw, uint32_t saveNew)
 {
     EncLds& L = sEnc;
     dst = uni(dst);
     lit = uni(lit);
     n = uni(n);
     writeRaw = uni(writeRaw);
+    prevCw = uni(prevCw);
+    prevCheck = uni(prevCheck);
+    nextCw = uni(nextCw);
+    saveNew = uni(saveNew);
+    auto ret = [](size_t sz, bool nt) { LitOut o; o.size = (uint32_t)sz; o.newTable = nt ? 1u : 0u; return o; };
     auto write_raw_literals_wave = [&](uint8_t* d, const uint8_t* l, uint32_t m) -> size_t {
         if (writeRaw) return pgn::write_raw_literals_wave(d, l, m);
         return z1::raw_lit_header_size(m) + m;
     };
     const int lane = lane_id();
-    if (n <= 63) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
+    if (n <= 63) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
     const uint32_t minGain = (n >> 6) + 2;
     const uint32_t lhSize = (uint32_t)z1::huf_lit_header_size(n);
     const bool single = n < 256;
@@ -1237,9 +1265,25 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
             z1::write_rawrle_lit_header(dst, n, z1::kSetRle);
             dst[fl] = lit[0];
         }
-        return fl + 1;
+        return ret(fl + 1, false);
     }
-    if (largest <= (n >> 7) + 4) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
+    if (largest <= (n >> 7) + 4) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
+    // HUF_validateCTable: the previous table must code every symbol present; a valid one is kept
+    // for small inputs (preferRepeat) or when it is estimated no worse than a new table + its header
+    uint32_t oldNb[4] = {0, 0, 0, 0};
+    bool repeat = false;
+    if (prevCheck) {
+        bool bad = false;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            oldNb[q] = gld<uint32_t>(prevCw + lane + 64 * q) >> 16;
+            bad |= c[q] != 0 && oldNb[q] == 0;
+        }
+        repeat = !ballot(bad);
+    }
+    bool useOld = repeat && n <= 1024;
+    uint32_t hSize = 0;
+    if (!useOld) {
     unsigned huffLog = z1::huf_optimal_table_log(z1::kHufTableLogDefault, n, maxSym);
     // HUF_sort: rank = #greater + #equal-with-smaller-symbol (stable, decreasing count)
     for (int i = lane; i < 2 * 256 + 4; i += 64) {
@@ -1278,9 +1322,23 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     for (int q = 0; q < 4; q++) nnz += (uint32_t)__builtin_popcountll(ballot(c[q] != 0));
     const uint32_t hl = huf_tree_wave(maxSym, huffLog, nnz, P);
     P.mark(14);
-    const uint32_t hSize = huf_write_ctable_wave(maxSym, hl, P);
+    hSize = huf_write_ctable_wave(maxSym, hl, P);
     P.mark(5);
-    if (hSize == 0 || hSize + 12 >= n) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
+    if (hSize == 0) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
+    if (repeat) {  // HUF_estimateCompressedSize of the old and the new table
+        uint32_t eo = 0, en = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int s = lane + 64 * q;
+            eo += c[q] * oldNb[q];
+            en += c[q] * (((uint32_t)s <= maxSym) ? (uint32_t)L.nbBits[s] : 0u);
+        }
+        const uint32_t oldSize = wave_sum(eo) >> 3, newSize = wave_sum(en) >> 3;
+        useOld = oldSize <= hSize + newSize || hSize + 12 >= n;
+    }
+    if (!useOld && hSize + 12 >= n) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
+    }  // !useOld
+    if (useOld) hSize = 0;  // a repeated table has no description
     // exact stream sizes from the segment histograms
     uint32_t bytes[4] = {0, 0, 0, 0}, bits[4] = {0, 0, 0, 0};
     {
@@ -1288,8 +1346,11 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             int s = lane + 64 * q;
-            uint32_t nbq = ((uint32_t)s <= maxSym) ? L.nbBits[s] : 0;
-            L.cw[s] = ((uint32_t)s <= maxSym) ? ((uint32_t)L.val[s] | (nbq << 16)) : 0;
+            uint32_t cwq;
+            if (useOld) cwq = gld<uint32_t>(prevCw + s);
+            else cwq = ((uint32_t)s <= maxSym) ? ((uint32_t)L.val[s] | ((uint32_t)L.nbBits[s] << 16)) : 0u;
+            L.cw[s] = cwq;
+            const uint32_t nbq = cwq >> 16;
 #pragma unroll
             for (int k = 0; k < 4; k++) b4[k] += seg_count(L, k, s) * nbq;
         }
@@ -1301,9 +1362,13 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
     }
     uint32_t cStreams = single ? bytes[0] : 6 + bytes[0] + bytes[1] + bytes[2] + bytes[3];
     uint32_t total = hSize + cStreams;
-    if (total >= n - 1 || total >= n - minGain) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return r; }
+    if (total >= n - 1 || total >= n - minGain) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
+    if (!useOld && saveNew) {  // the table a later block may repeat
+#pragma unroll
+        for (int q = 0; q < 4; q++) gst<uint32_t>(nextCw + lane + 64 * q, L.cw[lane + 64 * q]);
+    }
     if (lane == 0) {
-        z1::write_huf_lit_header(dst, lhSize, n, total, single);
+        z1::write_huf_lit_header(dst, lhSize, n, total, single, useOld ? z1::kSetRepeat : z1::kSetCompressed);
         if (!single) {
             z1::wr16(dst + lhSize + hSize, bytes[0]);
             z1::wr16(dst + lhSize + hSize + 2, bytes[1]);
@@ -1320,12 +1385,23 @@ __device__ __noinline__ size_t compress_literals_wave(uint8_t* __restrict__ dst,
         op += bytes[k];
     }
     P.mark(6);
-    return lhSize + total;
+    return ret(lhSize + total, !useOld);
 }
 
 // ---------------------------------------------------------------------------------------------
-// One stream -> one frame.  dst must have compress_bound(n) bytes.  Returns the frame size.
+// One stream -> one frame of up to kMaxFrameSrc bytes (ZSTD_compress_frameChunk: blocks of 128 KiB;
+// the block logic and the state a frame carries across its blocks -- hash table, repeat offsets,
+// Huffman table -- are zstd1_model.h compress_block).  dst must have compress_bound(n) bytes.
+// Returns the frame size.
 // ---------------------------------------------------------------------------------------------
+__device__ inline bool wave_is_rle(const uint8_t* p, uint32_t n)  // ZSTD_isRLE
+{
+    const uint8_t b0 = gb(p);
+    bool diff = false;
+    for (uint32_t i = (uint32_t)lane_id(); i < n; i += 64) diff |= gb(p + i) != b0;
+    return !ballot(diff);
+}
+
 __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
                                              EncScratch S, uint32_t tag, PhaseProf& P)
 {
@@ -1340,6 +1416,7 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
     S.seqSection = uni(S.seqSection);
     S.seqWork = uni(S.seqWork);
     S.maxSeq = uni(S.maxSeq);
+    S.huf = uni(S.huf);
     const int lane = lane_id();
     if (n == 0) {
         if (lane == 0) z1::write_empty_frame(dst);
@@ -1351,62 +1428,88 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         return h + 3 + n;
     }
     const z1::Params p = z1::level1_params(n);
-    const uint64_t sr = fast_search_wave(src, n, p.hashLog, p.mls, S.ht, tag, S.seqs);
-    const uint32_t nbSeq = (uint32_t)sr, lastLL = (uint32_t)(sr >> 32);
-    P.mark(1);
-    const uint8_t* lit = src;
-    uint32_t nLit = n;
-    if (nbSeq > 0) {
-        // gather the literal runs
-        uint32_t pos = 0, o = 0;
-        for (uint32_t i = 0; i < nbSeq; i++) {
-            const z1::Seq sq = S.seqs[i];
-            wave_copy(S.lit + o, src + pos, sq.litLength);
-            o += sq.litLength;
-            pos += sq.litLength + sq.mlBase + 3;
+    if (lane == 0) z1::write_frame_header(dst, n);
+    size_t o = h;
+    uint32_t rep0 = 1, rep1 = 4;  // confirmed repeat offsets (rep[2] is never read at level 1)
+    uint32_t hufCur = 0, hufCheck = 0;
+    for (uint32_t start = 0; start < n; start += (uint32_t)z1::kMaxSrc) {
+        const uint32_t bs = (n - start < (uint32_t)z1::kMaxSrc) ? n - start : (uint32_t)z1::kMaxSrc;
+        const bool last = start + bs == n, first = start == 0;
+        uint8_t* bdst = dst + o;
+        uint32_t cSize = 0;  // 0: raw block, 1: RLE block, else compressed body size
+        size_t seqSize = 0;
+        if (bs >= 7) {
+            const SearchOut so = fast_search_wave(src, start, start + bs, p.hashLog, p.mls, S.ht, tag, S.seqs, rep0, rep1);
+            const uint32_t nbSeq = uni(so.nbSeq), lastLL = uni(so.lastLL);
+            P.mark(1);
+            const uint8_t* lit = src + start;
+            uint32_t nLit = bs;
+            if (nbSeq > 0) {
+                // gather the literal runs
+                uint32_t pos = start, q = 0;
+                for (uint32_t i = 0; i < nbSeq; i++) {
+                    const z1::Seq sq = S.seqs[i];
+                    wave_copy(S.lit + q, src + pos, sq.litLength);
+                    q += sq.litLength;
+                    pos += sq.litLength + sq.mlBase + 3;
+                }
+                wave_copy(S.lit + q, src + pos, lastLL);
+                q += lastLL;
+                wave_sync();
+                lit = S.lit;
+                nLit = q;
+                P.mark(2);
+            }
+            uint8_t* body = bdst + 3;
+            // without sequences a raw literals section makes the block raw (lh + n + 1 >= maxCSize): it
+            // is then only sized here, and the raw block below is the one copy
+            const LitOut lo = compress_literals_wave(body, lit, nLit, P, nbSeq > 0 ? 1u : 0u, S.huf + 256 * hufCur, hufCheck,
+                                                     S.huf + 256 * (hufCur ^ 1u), last ? 0u : 1u);
+            const size_t litSize = uni(lo.size);
+            wave_sync();
+            if (nbSeq == 0) {
+                if (lane == 0) body[litSize] = 0;
+                seqSize = 1;
+            } else {
+                const size_t r = seq_section_wave(S, nbSeq);
+                seqSize = (r == (size_t)-1 || r == (size_t)-2) ? (size_t)-1 : r;
+                P.mark(8);
+            }
+            const size_t maxCSize = bs - ((bs >> 6) + 2);
+            if (seqSize != (size_t)-1 && litSize + seqSize < maxCSize) cSize = (uint32_t)(litSize + seqSize);
+            // a later block of one repeated byte is an RLE block (never the first: decoders <= 1.4.3)
+            if (!first && cSize < 25 && wave_is_rle(src + start, bs)) cSize = 1;
+            if (cSize > 1) {  // ZSTD_confirmRepcodesAndEntropyTables
+                rep0 = uni(so.rep0);
+                rep1 = uni(so.rep1);
+                if (uni(lo.newTable)) {
+                    hufCur ^= 1u;
+                    hufCheck = 1;
+                }
+            }
         }
-        wave_copy(S.lit + o, src + pos, lastLL);
-        o += lastLL;
         wave_sync();
-        lit = S.lit;
-        nLit = o;
-        P.mark(2);
-    }
-    uint8_t* body = dst + h + 3;
-    // without sequences a raw literals section makes the block raw (lh + n + 1 >= maxCSize): it is
-    // then only sized here, and the raw block below is the one copy
-    const size_t litSize = compress_literals_wave(body, lit, nLit, P, nbSeq > 0 ? 1u : 0u);
-    wave_sync();
-    size_t seqSize;
-    if (nbSeq == 0) {
-        if (lane == 0) body[litSize] = 0;
-        seqSize = 1;
-    } else {
-        const size_t r = seq_section_wave(S, nbSeq);
-        seqSize = (r == (size_t)-1 || r == (size_t)-2) ? (size_t)-1 : r;
-        P.mark(8);
-    }
-    const size_t maxCSize = n - ((n >> 6) + 2);
-    if (seqSize == (size_t)-1 || litSize + seqSize >= maxCSize) {
-        wave_sync();
-        if (lane == 0) {
-            z1::write_frame_header(dst, n);
-            z1::wr24(dst + h, (uint32_t)(1u + (z1::kBtRaw << 1) + (n << 3)));
+        size_t bsz;
+        if (cSize == 0) {
+            if (lane == 0) z1::wr24(bdst, (uint32_t)((last ? 1u : 0u) + (z1::kBtRaw << 1) + (bs << 3)));
+            wave_copy(bdst + 3, src + start, bs);
+            bsz = 3 + bs;
+        } else if (cSize == 1) {
+            if (lane == 0) {
+                z1::wr24(bdst, (uint32_t)((last ? 1u : 0u) + (z1::kBtRle << 1) + (bs << 3)));
+                bdst[3] = src[start];
+            }
+            bsz = 4;
+        } else {
+            if (seqSize > 1) wave_copy(bdst + 3 + (cSize - seqSize), S.seqSection, seqSize);
+            if (lane == 0) z1::wr24(bdst, (uint32_t)((last ? 1u : 0u) + (z1::kBtCompressed << 1) + (cSize << 3)));
+            bsz = 3 + cSize;
         }
-        wave_copy(dst + h + 3, src, n);
+        o += bsz;
         wave_sync();
         P.mark(9);
-        return h + 3 + n;
     }
-    if (nbSeq > 0) wave_copy(body + litSize, S.seqSection, seqSize);
-    const size_t cSize = litSize + seqSize;
-    if (lane == 0) {
-        z1::write_frame_header(dst, n);
-        z1::wr24(dst + h, (uint32_t)(1u + (z1::kBtCompressed << 1) + (cSize << 3)));
-    }
-    wave_sync();
-    P.mark(9);
-    return h + 3 + cSize;
+    return o;
 }
 
 }  // namespace pgn

@@ -33,19 +33,12 @@ def test_real_chunks_and_edge_sizes_identical(codecs, variant):
     c = codecs[variant]
     sigs = [O.vbz_decompress(b, n)[1] for b, n in real_vbz_chunks()]
     sigs += [O.synth_read(3000 + n, n) for n in [0, 1, 2, 3, 4, 5, 7, 8, 9, 255, 256, 257, 1023, 1024, 1025, 16385,
-                                                 65792, 102400, 131072]]
-    from rawnanoporesignalcompression_amd import PGNanoError
+                                                 65792, 102400, 131072, 131073, 200000, 262144]]
 
     for i, x in enumerate(sigs):
         rc, ref, _ = O.variant_compress(variant, x)
         assert rc == O.OK
-        if max(len(s) for s in O.variant_streams(variant, x)) > 128 * 1024:  # multi-block frame
-            with pytest.raises(PGNanoError) as ei:
-                c.compress_signal(x)
-            assert ei.value.status == 9
-            assert np.array_equal(c.decompress_signal(ref, sample_count=x.size), x), (variant, i)
-            continue
-        blob = c.compress_signal(x)
+        blob = c.compress_signal(x)  # streams above 128 KiB: multi-block frames
         assert blob == ref, (variant, i, x.size)
         assert np.array_equal(c.decompress_signal(blob, sample_count=x.size), x), (variant, i)
 
@@ -57,12 +50,7 @@ def test_pattern_signals(codecs, variant):
     c = codecs[variant]
     for name, x in _pattern_signals().items():
         rc, ref, _ = O.variant_compress(variant, x)
-        streams = O.variant_streams(variant, x)
-        if max(len(s) for s in streams) > 128 * 1024:  # multi-block frame: not on the GPU encoder
-            with pytest.raises(PGNanoError) as ei:
-                c.compress_signal(x)
-            assert ei.value.status == 9, (variant, name)
-        elif rc == O.OK:
+        if rc == O.OK:  # streams above 128 KiB included (multi-block frames)
             assert c.compress_signal(x) == ref, (variant, name)
         else:
             with pytest.raises(PGNanoError) as ei:
