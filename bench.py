@@ -325,6 +325,33 @@ def per_chunk_plugin(torch, codec, S, seed, nreads=200):
             "sample": f"{nreads} reads x {S} samples, one pgn_compress_signal / pgn_decompress_signal call each"}
 
 
+def pod5_batch_host(torch, codec, S, seed, nreads=1000):
+    """The batched POD5 integration (include/pgnano_pod5.h) on host memory: one
+    pod5_add_reads_data-shaped call (reads chunked at the writer's 102,400 samples, all chunks in one
+    launch, the packed signal column back) and the decode of those rows, PCIe transfers included."""
+    from rawnanoporesignalcompression_amd import Pod5SignalBatch
+
+    samples, _, _ = codec.synth_reads(nreads, S, seed=seed)
+    host = samples.cpu().numpy()
+    torch.cuda.synchronize()
+    reads = [host[r * S:(r + 1) * S] for r in range(nreads)]
+    b = Pod5SignalBatch(codec)
+    try:
+        offsets, data, smp, _ = b.compress_reads(reads[:8])  # warm the staging buffers
+        b.decompress_rows(offsets, data, smp)
+        t0 = time.perf_counter()
+        offsets, data, smp, _ = b.compress_reads(reads)
+        t1 = time.perf_counter()
+        b.decompress_rows(offsets, data, smp)
+        t2 = time.perf_counter()
+    finally:
+        b.close()
+    n = nreads * S
+    return {"encode_msamples_s": round(n / (t1 - t0) / 1e6, 1), "decode_msamples_s": round(n / (t2 - t1) / 1e6, 1),
+            "sample": f"{nreads} reads x {S} samples in one pgn_pod5_compress_reads / pgn_pod5_decompress_rows call, "
+                      "host memory (pageable in/out, pinned staging)"}
+
+
 # ---- roofline traffic evidence -------------------------------------------------------------------
 def source_digest() -> str:
     """sha256 over the kernel sources the measured library is built from (csrc/*.hip, csrc/*.h,
@@ -550,6 +577,7 @@ def main(argv=None):
         side["stream_copy_gbs"] = round(stream_copy_gbs(torch), 1)
         side["pcie_inclusive"] = pcie_inclusive(torch, codec, args.samples, args.seed)
         side["per_chunk_plugin"] = per_chunk_plugin(torch, codec, args.samples, args.seed)
+        side["pod5_batch_host"] = pod5_batch_host(torch, codec, args.samples, args.seed)
     line = run_rank(args, rank, world, local, codec, torch, dist, device=torch.device("cuda", dev_index))
     if line is not None:
         line.update(side)

@@ -9,6 +9,7 @@ from .codec import (
     EncodedBatch,
     PGNanoCodec,
     PGNanoError,
+    Pod5SignalBatch,
     VBZCodec,
     compress_signal,
     compressed_signal_max_size,
@@ -26,6 +27,7 @@ __all__ = [
     "PGN_MAX_CHUNK_SAMPLES",
     "PGNanoCodec",
     "PGNanoError",
+    "Pod5SignalBatch",
     "VBZCodec",
     "compress_signal",
     "compressed_signal_max_size",

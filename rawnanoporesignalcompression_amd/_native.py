@@ -26,6 +26,7 @@ PGN_ERR_INVALID_ARG = 10
 PGN_ERR_HIP = 11
 PGN_ERR_NO_DEVICE = 12
 
+PGN_POD5_CODEC_VBZ = 100  # include/pgnano_pod5.h
 PGN_MAX_CHUNK_SAMPLES = 262144
 # pgn_variant: the reference's compile-time COMPRESSOR_* variants (pgnano.cpp:70-92)
 VARIANTS = {"C5": 0, "C4": 1, "C1": 2, "C2": 3, "C3": 4, "VBZ0": 5}
@@ -68,6 +69,12 @@ SIGNATURES = [
     ("pgn_ctx_kernels", C.c_char_p, [_VP, C.c_int]),
     ("pgn_ctx_last_encode_ms", C.c_float, [_VP]),
     ("pgn_ctx_last_decode_ms", C.c_float, [_VP]),
+    # include/pgnano_pod5.h
+    ("pgn_pod5_batch_create", C.c_int, [_VP, C.c_int, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("pgn_pod5_batch_destroy", C.c_int, [_VP]),
+    ("pgn_pod5_compress_reads", C.c_int, [_VP, C.c_uint32, _VP, _VP, C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    ("pgn_pod5_decompress_rows", C.c_int, [_VP, C.c_uint32, _VP, _VP, _VP, _VP, _VP]),
 ]
 
 

@@ -352,3 +352,64 @@ def vbz_decompress_signal_capi(compressed, sample_count: int):
     _check(lib.pgn_pod5_vbz_decompress_signal(src.ctypes.data if src.size else 0, src.size, int(sample_count),
                                               out.ctypes.data))
     return out[: int(sample_count)]
+
+
+class Pod5SignalBatch:
+    """The batched POD5 signal-table integration (include/pgnano_pod5.h) on a codec's context.
+
+    ``compress_reads(reads)`` is the signal half of ``pod5_add_reads_data`` (c_api.cpp:1104-1129):
+    every read is chunked at ``chunk_size`` as the writer does (file_writer.cpp:119-143) and all
+    chunks are compressed by one batched launch; it returns the signal column the writer appends
+    (``offsets``, ``data``) with the per-chunk ``samples`` and ``read_index``.
+    ``decompress_rows(offsets, data, samples)`` decodes a record batch of signal rows
+    (signal_table_reader.cpp:294-318) into one int16 array."""
+
+    def __init__(self, codec: PGNanoCodec, chunk_size: int = 0):
+        self._codec = codec
+        self._lib = codec._lib
+        if isinstance(codec, VBZCodec):
+            cid = _native.PGN_POD5_CODEC_VBZ
+        else:
+            cid = _native.VARIANTS[codec.variant]
+        h = C.c_void_p()
+        _check(self._lib.pgn_pod5_batch_create(codec._h, cid, int(chunk_size), C.byref(h)))
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.pgn_pod5_batch_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compress_reads(self, reads):
+        xs = [np.ascontiguousarray(r, dtype=np.int16) for r in reads]
+        ptrs = (C.c_void_p * max(len(xs), 1))(*[x.ctypes.data if x.size else None for x in xs])
+        sizes = np.array([x.size for x in xs] or [0], dtype=np.uint32)
+        n = C.c_size_t(0)
+        po, pd, ps, pr = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        rc = self._lib.pgn_pod5_compress_reads(self._h, len(xs), ptrs, sizes.ctypes.data, C.byref(n), C.byref(po),
+                                               C.byref(pd), C.byref(ps), C.byref(pr))
+        _check(rc, f"chunk {n.value}" if rc else "")
+        k = n.value
+        offsets = np.ctypeslib.as_array((C.c_uint64 * (k + 1)).from_address(po.value)).copy()
+        data = (np.ctypeslib.as_array((C.c_uint8 * int(offsets[-1])).from_address(pd.value)).copy()
+                if offsets[-1] else np.zeros(0, np.uint8))
+        samples = np.ctypeslib.as_array((C.c_uint32 * k).from_address(ps.value)).copy() if k else np.zeros(0, np.uint32)
+        read_index = np.ctypeslib.as_array((C.c_uint32 * k).from_address(pr.value)).copy() if k else np.zeros(0, np.uint32)
+        return offsets, data, samples, read_index
+
+    def decompress_rows(self, offsets, data, samples):
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        samples = np.ascontiguousarray(samples, dtype=np.uint32)
+        k = samples.size
+        out = np.empty(max(int(samples.sum()), 1), dtype=np.int16)
+        st = np.zeros(max(k, 1), dtype=np.int32)
+        _check(self._lib.pgn_pod5_decompress_rows(self._h, k, offsets.ctypes.data, data.ctypes.data if data.size else None,
+                                                  samples.ctypes.data, out.ctypes.data, st.ctypes.data))
+        return out[: int(samples.sum())]

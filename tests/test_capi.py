@@ -9,9 +9,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    src = open(os.path.join(ROOT, "include", "pgnano_hip.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(pgn_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in ("pgnano_hip.h", "pgnano_pod5.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(pgn_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_header_symbols_exported_and_bound():
@@ -57,3 +60,18 @@ def test_missing_library_raises(tmp_path):
 
     with pytest.raises(NativeLibraryError):
         _native.load(str(tmp_path / "nope.so"))
+
+
+def test_c_program_builds_against_headers():
+    """tests/c/test_pod5_batch.c compiles against include/ and links with the product library; without a
+    GPU it reports the missing device (exit 77) instead of failing."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "rawnanoporesignalcompression_amd", "_build", "test_pod5_batch")
+    assert os.path.exists(exe), "build it with make -C rawnanoporesignalcompression_amd"
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: run by tests/test_gpu_pod5_batch.py")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 77, (r.returncode, r.stdout, r.stderr)
