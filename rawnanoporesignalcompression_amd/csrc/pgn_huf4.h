@@ -113,6 +113,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     hdbg(1, (uint32_t)k, (uint32_t)j, (uint32_t)T, (uint32_t)sl, nsym, tl, rs);
 #endif
     while (ballot(T > 0)) {
+        P.count(0);
         const int32_t hi = T - j * kWinBits;
         const int32_t lo = (hi - kWinBits > 0) ? hi - kWinBits : 0;
         const int32_t b8 = 8 * base;
@@ -140,12 +141,14 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             StgBits r;
             stg_init(r, lane, q - b8 - tli);
             while (ballot(q > hi)) {  // overlap: decoded, neither counted nor recorded
+                P.count(1);
                 uint32_t e[2];
                 stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
 #pragma unroll
                 for (int u = 0; u < 2; u++) q = q > hi ? q - (int32_t)(e[u] >> 8) : q;
             }
             while (ballot(q > lo && hi - q < kBmpBits)) {
+                P.count(2);
                 uint32_t e[2];
                 stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
 #pragma unroll
@@ -161,6 +164,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             }
             // every active lane has >= 4 * tl bits left: four symbols without a bound check
             while (ballot(q > lo) && !ballot(q > lo && q - lo < 4 * tli)) {
+                P.count(3);
                 const bool act = q > lo;
                 int32_t qq = q;
 #pragma unroll
@@ -173,6 +177,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 c += act ? 4u : 0u;
             }
             while (ballot(q > lo)) {
+                P.count(4);
 #pragma unroll
                 for (int v = 0; v < 2; v++) {
                     uint32_t e[2];
@@ -195,6 +200,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         int32_t ex = q;
         bool need = j > 0;
         for (int it = 0; it < 16; it++) {
+            P.count(5);
             if (need) {
                 int32_t p = entry;
                 uint32_t w = 0;
@@ -226,6 +232,9 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                     ex = p;
                 }
             }
+#ifdef PGN_PROFILE
+            P.count(6, wave_max(need ? cnt : 0u) > 0 ? 1u : 0u);  // sync iterations with any walking lane
+#endif
             const int32_t prevEx = (int32_t)dpp<kDppRowShr1>((uint32_t)ex);
             const int32_t ne = (j == 0) ? hi : prevEx;
             need = (j > 0) && (ne != entry);
@@ -254,6 +263,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             stg_init(r, lane, p - b8 - tli);
             uint32_t i = 0;
             while (ballot(i + 4 <= cnt)) {
+                P.count(7);
                 if (i + 4 <= cnt) {
                     uint32_t word = 0;
 #pragma unroll
@@ -268,6 +278,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 }
             }
             while (ballot(i < cnt)) {
+                P.count(8);
                 if (i < cnt) {
                     const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
                     p -= (int32_t)(e >> 8);

@@ -695,6 +695,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
             continue;
         }
         P.mark(0);
+        P.count(9, (n + 1023) / 1024);
         wave_sync();
         uint8_t* dst = a.out + a.outOffsets[c];
         const uint64_t cap = a.outCaps[c];
@@ -1068,8 +1069,9 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     const char* pe = getenv("PGN_PHASE_PROFILE");
     if (pe && pe[0] == '1') {
-        HIPCHK(hipMalloc(&c->prof, 2 * kPhases * sizeof(uint64_t)));
-        HIPCHK(hipMemset(c->prof, 0, 2 * kPhases * sizeof(uint64_t)));
+        // [encode phases][decode phases][encode counters][decode counters]
+        HIPCHK(hipMalloc(&c->prof, 2 * (kPhases + kCounters) * sizeof(uint64_t)));
+        HIPCHK(hipMemset(c->prof, 0, 2 * (kPhases + kCounters) * sizeof(uint64_t)));
         HIPCHK(hipDeviceSynchronize());
     }
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
@@ -1547,13 +1549,14 @@ int pgn_debug_huf_dump(uint32_t* out, size_t nwords)
 int pgn_debug_phase_cycles(pgn_ctx* c, uint64_t* out, int n)
 {
     if (!c || !out || n < 2 * kPhases) return PGN_ERR_INVALID_ARG;
+    const int m = n < 2 * (kPhases + kCounters) ? n : 2 * (kPhases + kCounters);
     if (!c->prof) {
-        memset(out, 0, sizeof(uint64_t) * 2 * kPhases);
+        memset(out, 0, sizeof(uint64_t) * m);
         return PGN_OK;
     }
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpy(out, c->prof, sizeof(uint64_t) * 2 * kPhases, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, c->prof, sizeof(uint64_t) * m, hipMemcpyDeviceToHost));
     return PGN_OK;
 }
 

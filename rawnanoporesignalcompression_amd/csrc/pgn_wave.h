@@ -196,15 +196,18 @@ __device__ inline void wave_fill(uint8_t* dst, uint8_t v, size_t n)
 // accumulate per phase; lane 0 adds them to a global buffer at kernel end.
 // ---------------------------------------------------------------------------------------------
 constexpr int kPhases = 16;
+constexpr int kCounters = 16;  // event counters (loop trip counts) after the phase cycles
 struct PhaseProf {
 #ifdef PGN_PROFILE
     uint64_t* out;
     uint64_t last;
     uint64_t acc[kPhases];
+    uint64_t cnt[kCounters];
     __device__ void init(uint64_t* o)
     {
         out = o;
         for (int i = 0; i < kPhases; i++) acc[i] = 0;
+        for (int i = 0; i < kCounters; i++) cnt[i] = 0;
         last = o ? __builtin_amdgcn_s_memtime() : 0;
     }
     __device__ __forceinline__ void mark(int phase)
@@ -215,14 +218,23 @@ struct PhaseProf {
             last = t;
         }
     }
+    // wave-level event count (call with wave-uniform control flow)
+    __device__ __forceinline__ void count(int k, uint64_t v = 1)
+    {
+        if (out) cnt[k] += v;
+    }
     __device__ void flush()
     {
-        if (out && lane_id() == 0)
+        if (out && lane_id() == 0) {
             for (int i = 0; i < kPhases; i++) atomicAdd((unsigned long long*)&out[i], (unsigned long long)acc[i]);
+            for (int i = 0; i < kCounters; i++)
+                atomicAdd((unsigned long long*)&out[2 * kPhases + i], (unsigned long long)cnt[i]);
+        }
     }
 #else
     __device__ __forceinline__ void init(uint64_t*) {}
     __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void count(int, uint64_t = 1) {}
     __device__ __forceinline__ void flush() {}
 #endif
 };

@@ -899,6 +899,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
         hpos += fcsSize;
         ip = hpos;
         const size_t frameStart = op;
+        P.count(13);
         bool hufValid = false;  // a Huffman table exists for treeless literals
         bool hufInLds = false;  // ... and is in sDec.tab (tables up to kHufLdsLog)
         bool hufParked = false; // ... and a copy is parked in S.htab
@@ -910,12 +911,14 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
             const uint32_t bh = hw_u24(hw, src, ip);
             ip += 3;
             const unsigned last = bh & 1, btype = (bh >> 1) & 3;
+            P.count(12);
             const size_t bsize = bh >> 3;
             if (btype == 3) return z1::kDecErrCorrupt;
             if (btype == z1::kBtRaw) {
                 if (bsize > srcSize - ip) return z1::kDecErrSrcSmall;
                 if (op + bsize > dstCap) return z1::kDecErrDstSmall;
                 wave_copy8(dst + op, src + ip, bsize);
+                P.count(14, bsize);
                 ip += bsize;
                 op += bsize;
                 P.mark(5);
@@ -970,6 +973,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     if (ltype == z1::kSetCompressed) {
                         unsigned tlNew = 0;
                         const size_t hsz = huf_build_dtable_wave(hp, remain, &tlNew, S.htab);
+                        P.count(9);
                         P.mark(1);
                         if (hsz == 0) return z1::kDecErrHufTable;
                         hufValid = true;
@@ -1016,6 +1020,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     hufInLds = false;
                     wave_sync();
                     const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, last != 0, fs);
+                    P.count(11);
                     if (r < 0) return r;
                     op = (size_t)r;
                     P.mark(4);

@@ -164,7 +164,7 @@ __device__ inline uint32_t wave_back_count(const uint8_t* src, uint32_t a, uint3
 // Searches the block [start, end) of src (table and positions frame-wide, zstd1_model.h
 // fast_search_serial); rep0 / rep1 are the confirmed repeat offsets on entry.
 struct SearchOut {
-    uint32_t nbSeq, lastLL, rep0, rep1;
+    uint32_t nbSeq, lastLL, rep0, rep1, rounds;
 };
 __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ src, uint32_t start, uint32_t end, unsigned hlog,
                                                    unsigned mls, uint32_t* __restrict__ ht, uint32_t tag,
@@ -188,7 +188,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     uint32_t off1 = rep0, off2 = rep1, offSaved = 0;
     if (off2 > (uint32_t)ip0) { offSaved = off2; off2 = 0; }
     if (off1 > (uint32_t)ip0) { offSaved = off1; off1 = 0; }
-    uint32_t nbSeq = 0;
+    uint32_t nbSeq = 0, rounds = 0;
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
     lds_sync();
@@ -214,6 +214,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     };
     bool havePk = false;  // pk / pNext / v8 / repw already hold this round's visits (from the last round)
     while (ip0 + 1 < ilimit) {
+        rounds++;
         if (!havePk) {
             positions(ip0, pk, pNext);
             loads(pk, v8, repw);
@@ -374,6 +375,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     r.lastLL = (uint32_t)(iend - anchor);
     r.rep0 = off1 ? off1 : offSaved;
     r.rep1 = off2 ? off2 : offSaved;
+    r.rounds = rounds;
     return r;
 }
 
@@ -499,6 +501,8 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
     constexpr int kStart = z1::kHufStartNode;
     const int nonNullRank = (int)nnz - 1;
     const int nodeRoot = kStart + nonNullRank - 1;
+    P.count(2);
+    P.count(3, (uint64_t)(nodeRoot - kStart));
     L.nodes[0].count = 1u << 31;  // huffNode0[0]: barrier below the leaves
     // ---- create parents (two queues: leaves ascending from lowS down, nodes from lowN up)
     int lowS = nonNullRank, lowN = kStart, nodeNb = kStart;
@@ -577,6 +581,7 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
             L.tdep[lane + 64 * j] = (uint16_t)nd[j];
         }
         lds_sync();
+        P.count(4);
         if (!ballot(more)) break;
     }
     // leaves: parent depth + 1
@@ -1244,6 +1249,7 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
         }
     }
     wave_sync();
+    P.count(8, (n + 4095) / 4096);
     uint32_t c[4];
     uint32_t myMaxSym = 0, myLargest = 0;
 #pragma unroll
@@ -1323,6 +1329,8 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     const uint32_t hl = huf_tree_wave(maxSym, huffLog, nnz, P);
     P.mark(14);
     hSize = huf_write_ctable_wave(maxSym, hl, P);
+    P.count(5);
+    P.count(6, maxSym);
     P.mark(5);
     if (hSize == 0) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
     if (repeat) {  // HUF_estimateCompressedSize of the old and the new table
@@ -1382,6 +1390,7 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
         uint32_t a = segSize * (uint32_t)k;
         uint32_t e = (k == nseg - 1) ? n : a + segSize;
         huf_encode_segment_wave(op, lit + a, e - a, bits[k]);
+        P.count(7, (e - a + 1023) / 1024);
         op += bytes[k];
     }
     P.mark(6);
@@ -1428,6 +1437,7 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         return h + 3 + n;
     }
     const z1::Params p = z1::level1_params(n);
+    P.count(12);
     if (lane == 0) z1::write_frame_header(dst, n);
     size_t o = h;
     uint32_t rep0 = 1, rep1 = 4;  // confirmed repeat offsets (rep[2] is never read at level 1)
@@ -1442,6 +1452,9 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
             const SearchOut so = fast_search_wave(src, start, start + bs, p.hashLog, p.mls, S.ht, tag, S.seqs, rep0, rep1);
             const uint32_t nbSeq = uni(so.nbSeq), lastLL = uni(so.lastLL);
             P.mark(1);
+            P.count(0, uni(so.rounds));
+            P.count(1, nbSeq);
+            P.count(13);
             const uint8_t* lit = src + start;
             uint32_t nLit = bs;
             if (nbSeq > 0) {
@@ -1471,6 +1484,8 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
                 if (lane == 0) body[litSize] = 0;
                 seqSize = 1;
             } else {
+                P.count(10);
+                P.count(11, nbSeq);
                 const size_t r = seq_section_wave(S, nbSeq);
                 seqSize = (r == (size_t)-1 || r == (size_t)-2) ? (size_t)-1 : r;
                 P.mark(8);

@@ -22,11 +22,26 @@ enc = c.compress_batch(samples, offs, cnt)
 out, so, st = c.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
 torch.cuda.synchronize()
 print("encode ms", c.last_encode_ms(), "decode ms", c.last_decode_ms(), "ok", bool(torch.equal(out, samples)))
-buf = np.zeros(32, np.uint64)
-c._lib.pgn_debug_phase_cycles(c._h, buf.ctypes.data, 32)
+buf = np.zeros(64, np.uint64)
+c._lib.pgn_debug_phase_cycles(c._h, buf.ctypes.data, 64)
 for name, lab, arr in (("encode", ENC, buf[:16]), ("decode", DEC, buf[16:])):
     tot = float(arr.sum())
     print(f"{name}: total {tot/1e9:.2f} Gcycles (summed over waves), per chunk {tot/R/1e3:.1f} kcycles")
     for i, l in enumerate(lab):
         if arr[i]:
             print(f"   {l:18s} {100*arr[i]/tot:6.2f}%  {arr[i]/R/1e3:9.1f} kcyc/chunk")
+
+DCNT = ["huf rounds", "passA overlap iters", "passA bitmap iters", "passA main4 iters", "passA tail iters",
+        "sync iters", "sync iters with walks", "passB 4-sym iters", "passB 1-sym iters", "huf tables",
+        "-", "seq blocks", "blocks", "frames", "raw bytes", "-"]
+print("decode counters per chunk:")
+for i, l in enumerate(DCNT):
+    if buf[48 + i]:
+        print(f"   {l:24s} {buf[48 + i] / R:12.2f}")
+ECNT = ["search rounds", "sequences found", "tree builds", "tree merges", "depth iters", "writeCTable",
+        "ctable symbols", "huf encode steps", "hist iters", "split steps", "seq sections", "seqs encoded",
+        "frames", "blocks", "-", "-"]
+print("encode counters per chunk:")
+for i, l in enumerate(ECNT):
+    if buf[32 + i]:
+        print(f"   {l:24s} {buf[32 + i] / R:12.2f}")
