@@ -502,46 +502,93 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
     const int nonNullRank = (int)nnz - 1;
     const int nodeRoot = kStart + nonNullRank - 1;
     P.count(2);
-    P.count(3, (uint64_t)(nodeRoot - kStart));
     L.nodes[0].count = 1u << 31;  // huffNode0[0]: barrier below the leaves
-    // ---- create parents (two queues: leaves ascending from lowS down, nodes from lowN up)
+    // ---- create parents in rounds of independent merges.  The two-queue merge (leaves ascending
+    // from lowS down, nodes hn[lowN .. nodeNb) in creation order, a leaf taken only when strictly
+    // smaller) creates nodes of nondecreasing count, so with s = the sum of the next two picks, every
+    // queued node (<= s) and every leaf < s is picked before the node of count s is: those t
+    // elements, merged in pick order, form floor(t / 2) nodes at once -- node nodeNb + k from picks
+    // 2k and 2k + 1, exactly the serial loop's nodes.  An odd last element starts the next round.
+    // Pick positions: a leaf's is its rank plus the queued nodes <= it, a node's its rank plus the
+    // leaves < it (binary searches over the two sorted runs in LDS).
+    uint32_t* pickVal = L.count;  // dead after the sort
     int lowS = nonNullRank, lowN = kStart, nodeNb = kStart;
-    const uint32_t c0 = hn[lowS].count + hn[lowS - 1].count;
-    hn[nodeNb].count = c0;
-    hn[lowS].parent = (uint16_t)nodeNb;
-    hn[lowS - 1].parent = (uint16_t)nodeNb;
-    nodeNb++;
-    lowS -= 2;
-    uint32_t S0 = lowS >= 0 ? hn[lowS].count : (1u << 31);
-    uint32_t S1 = lowS >= 1 ? hn[lowS - 1].count : (1u << 31);
-    uint32_t Q0 = c0, Q1 = 1u << 30;  // uncreated nodes read 1 << 30, as in the reference
+    uint32_t rounds = 0;
     while (nodeNb <= nodeRoot) {
-        int nn[2];
-        uint32_t vv[2];
+        rounds++;
+        uint32_t s;
+        {
+            const uint32_t S0 = lowS >= 0 ? hn[lowS].count : (1u << 31);
+            const uint32_t S1 = lowS >= 1 ? hn[lowS - 1].count : (1u << 31);
+            const uint32_t Q0 = lowN < nodeNb ? hn[lowN].count : (1u << 30);
+            const uint32_t Q1 = lowN + 1 < nodeNb ? hn[lowN + 1].count : (1u << 30);
+            s = (S0 < Q0) ? S0 + (S1 < Q0 ? S1 : Q0) : Q0 + (S0 < Q1 ? S0 : Q1);
+        }
+        const uint32_t nq = (uint32_t)(nodeNb - lowN);
+        // leaves < s: a run ending at lowS (ascending rank i = leaf lowS - i)
+        const int leafSlots = (lowS + 64) >> 6;
+        uint32_t nl = 0;
+        uint32_t lv[4];
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            if (S0 < Q0) {
-                nn[k] = lowS;
-                vv[k] = S0;
-                lowS--;
-                S0 = S1;
-                S1 = lowS >= 1 ? hn[lowS - 1].count : (1u << 31);
-            } else {
-                nn[k] = lowN;
-                vv[k] = Q0;
-                lowN++;
-                Q0 = Q1;
-                Q1 = (lowN + 1 < nodeNb) ? hn[lowN + 1].count : (1u << 30);
+        for (int j = 0; j < 4; j++) {
+            lv[j] = 0xFFFFFFFFu;
+            if (j < leafSlots) {
+                const int i = lane + 64 * j;
+                if (i <= lowS) lv[j] = hn[lowS - i].count;
+                nl += (uint32_t)__builtin_popcountll(ballot(lv[j] < s));
             }
         }
-        const uint32_t cn = vv[0] + vv[1];
-        hn[nodeNb].count = cn;
-        hn[nn[0]].parent = (uint16_t)nodeNb;
-        hn[nn[1]].parent = (uint16_t)nodeNb;
-        if (lowN == nodeNb) Q0 = cn;
-        else if (lowN + 1 == nodeNb) Q1 = cn;
-        nodeNb++;
+        nl = uni(nl);
+        const uint32_t t = nl + nq, pairs = t >> 1, used = 2 * pairs;
+        uint32_t usedLeaves = 0;
+        const uint32_t stN = nq ? (1u << (31 - __builtin_clz(nq))) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (j < leafSlots) {
+                const uint32_t i = (uint32_t)lane + 64u * (uint32_t)j;
+                uint32_t lo = 0;
+                for (uint32_t st = stN; st; st >>= 1) {
+                    const uint32_t k = lo + st;
+                    if (k <= nq && hn[lowN + (int)k - 1].count <= lv[j]) lo = k;
+                }
+                const uint32_t pos = i + lo;
+                const bool take = i < nl && pos < used;
+                if (take) {
+                    hn[lowS - (int)i].parent = (uint16_t)(nodeNb + (int)(pos >> 1));
+                    pickVal[pos] = lv[j];
+                }
+                usedLeaves += (uint32_t)__builtin_popcountll(ballot(take));
+            }
+        }
+        const uint32_t stL = nl ? (1u << (31 - __builtin_clz(nl))) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (64u * (uint32_t)j < nq) {
+                const uint32_t m = (uint32_t)lane + 64u * (uint32_t)j;
+                if (m < nq) {
+                    const uint32_t v = hn[lowN + (int)m].count;
+                    uint32_t lo = 0;
+                    for (uint32_t st = stL; st; st >>= 1) {
+                        const uint32_t k = lo + st;
+                        if (k <= nl && hn[lowS - (int)k + 1].count < v) lo = k;
+                    }
+                    const uint32_t pos = m + lo;
+                    if (pos < used) {
+                        hn[lowN + (int)m].parent = (uint16_t)(nodeNb + (int)(pos >> 1));
+                        pickVal[pos] = v;
+                    }
+                }
+            }
+        }
+        lds_sync();
+        for (uint32_t k = (uint32_t)lane; k < pairs; k += 64) hn[nodeNb + (int)k].count = pickVal[2 * k] + pickVal[2 * k + 1];
+        lds_sync();
+        usedLeaves = uni(usedLeaves);
+        lowS -= (int)usedLeaves;
+        lowN += (int)(used - usedLeaves);
+        nodeNb += (int)pairs;
     }
+    P.count(3, rounds);
     lds_sync();
     P.mark(11);
     // ---- depths of the internal nodes: pointer jumping (distance to ancestor, ancestor of ancestor)

@@ -38,7 +38,7 @@ print("decode counters per chunk:")
 for i, l in enumerate(DCNT):
     if buf[48 + i]:
         print(f"   {l:24s} {buf[48 + i] / R:12.2f}")
-ECNT = ["search rounds", "sequences found", "tree builds", "tree merges", "depth iters", "writeCTable",
+ECNT = ["search rounds", "sequences found", "tree builds", "tree merge rounds", "depth iters", "writeCTable",
         "ctable symbols", "huf encode steps", "hist iters", "split steps", "seq sections", "seqs encoded",
         "frames", "blocks", "-", "-"]
 print("encode counters per chunk:")
