@@ -1086,6 +1086,9 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     // the predefined sequence FSE tables of the decoder (one wave, once per context)
     hipLaunchKernelGGL(seq_default_tables_kernel, dim3(1), dim3(64), 0, c->stream);
     HIPCHK(hipGetLastError());
+    // and the encoder's
+    hipLaunchKernelGGL(seq_default_ctables_kernel, dim3(1), dim3(64), 0, c->stream);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     *out = c;
     return PGN_OK;

@@ -192,16 +192,18 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
     lds_sync();
-    // positions of the 64 visits starting at p (the no-match recurrence; scalar, with v_writelane)
+    // positions of the 64 visits starting at p (the no-match recurrence q += ((q - anchor) >> 7) + 2;
+    // scalar, with v_writelane).  With e = q - anchor + 256 it is e += e >> 7: two scalar
+    // instructions per visit.
     auto positions = [&](int32_t p, int32_t& pkOut, int32_t& pNextOut) {
-        int32_t q = p, pk = 0;
+        uint32_t e = (uint32_t)(p - anchor) + 256u, ek = 0;
 #pragma unroll
         for (int k = 0; k < 64; k++) {
-            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(pk) : "s"(q), "i"(k));
-            q += ((q - anchor) >> 7) + 2;
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(ek) : "s"(e), "i"(k));
+            e += e >> 7;
         }
-        pkOut = pk;
-        pNextOut = q;
+        pkOut = (int32_t)ek + (anchor - 256);
+        pNextOut = (int32_t)e + (anchor - 256);
     };
     int32_t pk = 0, pNext = 0;
     uint64_t v8 = 0;    // bytes pk .. pk+7: both hashes and the current-position words
@@ -1072,6 +1074,27 @@ __device__ __forceinline__ void sfse_encode(GBitW& bw, uint32_t& st, const z1::F
     st = ct.stateTable[(st >> nbBitsOut) + ct.deltaFindState[symbol]];
 }
 
+// the predefined LL / OF / ML compression tables (kSetBasic), built once per context
+__device__ z1::FseCTable gSeqDefCT[3];
+static_assert(sizeof(z1::FseCTable) % 4 == 0, "word copy");
+__global__ __launch_bounds__(64) void seq_default_ctables_kernel()
+{
+    EncLds& L = sEnc;
+    const int lane = lane_id();
+#pragma unroll 1
+    for (int k = 0; k < 3; k++) {
+        const unsigned dmax = k == 0 ? z1::kMaxLL : (k == 1 ? z1::kDefaultMaxOff : z1::kMaxML);
+        const unsigned lg = k == 0 ? z1::kLLDefaultNormLog : (k == 1 ? z1::kOFDefaultNormLog : z1::kMLDefaultNormLog);
+        if ((unsigned)lane <= dmax)
+            L.snorm[lane] = k == 0 ? z1::ll_default_norm(lane) : (k == 1 ? z1::of_default_norm(lane) : z1::ml_default_norm(lane));
+        lds_sync();
+        fse_build_ctable_lds(L.sct[k], L.snorm, dmax, lg, L.stsym, L.scumul);
+        const uint32_t* w = (const uint32_t*)&L.sct[k];
+        for (uint32_t u = (uint32_t)lane; u < sizeof(z1::FseCTable) / 4; u += 64) ((uint32_t*)&gSeqDefCT[k])[u] = w[u];
+        lds_sync();
+    }
+}
+
 __device__ __noinline__ size_t seq_section_wave(EncScratch S, uint32_t nbSeq)
 {
     EncLds& L = sEnc;
@@ -1125,7 +1148,6 @@ __device__ __noinline__ size_t seq_section_wave(EncScratch S, uint32_t nbSeq)
     const unsigned maxes[3] = {z1::kMaxLL, z1::kMaxOff, z1::kMaxML};
     const unsigned fseLogs[3] = {z1::kLLFSELog, z1::kOffFSELog, z1::kMLFSELog};
     const unsigned normLogs[3] = {z1::kLLDefaultNormLog, z1::kOFDefaultNormLog, z1::kMLDefaultNormLog};
-    const unsigned defMax[3] = {z1::kMaxLL, z1::kDefaultMaxOff, z1::kMaxML};
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const uint32_t cnt = (lane <= maxes[k]) ? L.scount[k][lane] : 0u;
@@ -1144,11 +1166,9 @@ __device__ __noinline__ size_t seq_section_wave(EncScratch S, uint32_t nbSeq)
             ct.deltaFindState[mx] = 0;
             if (lane == 0) gst<uint8_t>(op, (uint8_t)lastCode[k]);
             op += 1;
-        } else if (type == z1::kSetBasic) {
-            if (lane <= defMax[k])
-                L.snorm[lane] = k == 0 ? z1::ll_default_norm(lane) : (k == 1 ? z1::of_default_norm(lane) : z1::ml_default_norm(lane));
-            lds_sync();
-            fse_build_ctable_lds(ct, L.snorm, defMax[k], normLogs[k], L.stsym, L.scumul);
+        } else if (type == z1::kSetBasic) {  // the predefined table, built once (seq_default_ctables_kernel)
+            const uint32_t* w = (const uint32_t*)&gSeqDefCT[k];
+            for (uint32_t u = lane; u < sizeof(z1::FseCTable) / 4; u += 64) ((uint32_t*)&ct)[u] = gld<uint32_t>(w + u);
         } else {
             size_t nbSeq_1 = nbSeq;
             const unsigned tableLog = z1::fse_optimal_table_log(fseLogs[k], nbSeq, mx, 2);

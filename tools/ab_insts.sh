@@ -1,6 +1,7 @@
 #!/bin/bash
 # Instruction counts per chunk of the codec kernels for each library build under ab/*.so (run via
 # gpurun): one rocprofv3 PMC pass (SQ_INSTS_VALU / SALU / LDS) over a 20,000-chunk encode+decode.
+# The environment passes through (PGN_ENC_PIPELINE=staged splits the encode into its three kernels).
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/abi
 R=${1:-20000}
@@ -17,9 +18,9 @@ for f in glob.glob(f"gpurun_out/abi/{n}/**/*counter_collection.csv", recursive=T
         k = r["Kernel_Name"].split("(")[0].split("::")[-1]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
 out = []
-for k in ("enc_chunk_kernel<0>", "dec_zstd_kernel", "dec_merge_kernel"):
-    v = agg.get(k)
-    if v:
+for k in sorted(agg):
+    v = agg[k]
+    if v['SQ_INSTS_VALU'] > 1e6:
         out.append(f"{k}: V {v['SQ_INSTS_VALU']/R/1e3:.1f}k S {v['SQ_INSTS_SALU']/R/1e3:.1f}k L {v['SQ_INSTS_LDS']/R/1e3:.1f}k")
 print(n, " | ".join(out))
 PY
