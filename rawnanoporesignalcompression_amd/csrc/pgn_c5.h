@@ -36,7 +36,32 @@ struct SplitLds {
     alignas(16) uint8_t M[kWinBytes + 256];
     alignas(16) uint8_t L[kWinBytes];
     alignas(16) uint8_t H[kWinBytes];
+    alignas(16) uint32_t Z[64 * 8];  // a lane's 16 zig-zag values (two per word), for its class-3 samples
 };
+
+typedef uint16_t pgn_u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t pgn_s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pgn_u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(pgn_u16x2, w); }
+__device__ __forceinline__ uint32_t as_u32(pgn_u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// packed 16-bit min / saturating subtract / wrapping subtract (one VOP3P instruction each)
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "s"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_subsat_u16(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_sub_u16 %0, %1, %2 clamp" : "=v"(r) : "v"(a), "s"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_sub_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // 4 nibble-bytes (each < 16) -> their 16-bit little-endian nibble packing
 __device__ __forceinline__ uint32_t pack_nibbles(uint32_t w)
@@ -90,75 +115,109 @@ template <bool C4> struct ClassOffsets {
 
 // One 1024-sample step (Full: every sample of the step exists).  Returns the lane's key word.
 // Full steps take the lane's 32 sample bytes already loaded (a, b: prefetched one step ahead).
+// Deltas, zig-zag and classes are computed two samples per instruction (packed 16-bit halves):
+// class = (v >= 1) + (v > t1) + (v > t2) from saturating subtracts.
 template <bool Full, bool C4 = false>
 __device__ __forceinline__ uint32_t split_step(const uint4& a, const uint4& b, const int16_t* __restrict__ x, uint32_t n,
                                                uint32_t t, SplitLds& W, uint32_t& fS, uint32_t& fM, uint32_t& fL,
                                                uint32_t& prevX)
 {
+    using CO = ClassOffsets<C4>;
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t i0 = t + 16u * lane;
-    uint32_t xv[16];
+    uint32_t wd[8];
     if (Full) {
-        const uint32_t wd[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            xv[2 * k] = wd[k] & 0xFFFFu;
-            xv[2 * k + 1] = wd[k] >> 16;
-        }
+        wd[0] = a.x; wd[1] = a.y; wd[2] = a.z; wd[3] = a.w;
+        wd[4] = b.x; wd[5] = b.y; wd[6] = b.z; wd[7] = b.w;
     } else {
 #pragma unroll
-        for (int m = 0; m < 16; m++) xv[m] = (i0 + (uint32_t)m < n) ? (uint32_t)gld<uint16_t>(x + i0 + m) : 0u;
+        for (int k = 0; k < 8; k++) {
+            const uint32_t lo = (i0 + 2u * k < n) ? (uint32_t)gld<uint16_t>(x + i0 + 2 * k) : 0u;
+            const uint32_t hi = (i0 + 2u * k + 1u < n) ? (uint32_t)gld<uint16_t>(x + i0 + 2 * k + 1) : 0u;
+            wd[k] = lo | (hi << 16);
+        }
     }
     // the sample before mine: lane l-1's last one (lane 0: the previous step's)
-    uint32_t prv = dpp<kDppWaveShr1>(xv[15]);
+    uint32_t prv = dpp<kDppWaveShr1>(wd[7] >> 16);
     prv = (lane == 0) ? prevX : prv;
-    prevX = readlane_u32(xv[15], 63);
-    uint32_t v[16];
-    uint32_t kw = 0;
+    prevX = readlane_u32(wd[7] >> 16, 63);
+    constexpr uint32_t kOne = 0x00010001u, kT1 = CO::t1 * kOne, kT2 = CO::t2 * kOne;
+    // stage by stage over the 8 pairs, so that dependent packed instructions are never adjacent
+    uint32_t z[8], val[8], cp[8], c2[8], c3[8];
 #pragma unroll
-    for (int m = 0; m < 16; m++) {
-        v[m] = zz_enc16((uint16_t)(xv[m] - prv));
-        prv = xv[m];
-        const bool valid = Full || (i0 + (uint32_t)m < n);
-        const uint32_t c = (valid && v[m] != 0) ? 1u + (v[m] > ClassOffsets<C4>::t1) + (v[m] > ClassOffsets<C4>::t2) : 0u;
-        kw |= c << (2 * m);
+    for (int k = 0; k < 8; k++) {
+        const uint32_t before = (k == 0) ? ((wd[0] << 16) | prv) : __builtin_amdgcn_alignbit(wd[k], wd[k - 1], 16);
+        const pgn_u16x2 d = as_u16x2(wd[k]) - as_u16x2(before);
+        z[k] = as_u32((d << (pgn_u16x2){1, 1}) ^ __builtin_bit_cast(pgn_u16x2, __builtin_bit_cast(pgn_s16x2, d) >> (pgn_s16x2){15, 15}));
     }
-    // places: step fills + the classes of the lanes below + my own running ranks
+#pragma unroll
+    for (int k = 0; k < 8; k++) c2[k] = pk_subsat_u16(z[k], kT1);
+#pragma unroll
+    for (int k = 0; k < 8; k++) c3[k] = pk_subsat_u16(z[k], kT2);
+#pragma unroll
+    for (int k = 0; k < 8; k++) cp[k] = pk_min_u16(z[k], kOne);
+#pragma unroll
+    for (int k = 0; k < 8; k++) c2[k] = pk_min_u16(c2[k], kOne);
+#pragma unroll
+    for (int k = 0; k < 8; k++) c3[k] = pk_min_u16(c3[k], kOne);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        cp[k] += c2[k] + c3[k];  // halves <= 3: no carry between them
+        if (!Full) {
+            const uint32_t vm = ((i0 + 2u * k < n) ? 0xFFFFu : 0u) | ((i0 + 2u * k + 1u < n) ? 0xFFFF0000u : 0u);
+            cp[k] &= vm;
+        }
+    }
+    // the byte a class-1 / class-2 sample stores: v - o1 or v - o2
+#pragma unroll
+    for (int k = 0; k < 8; k++) val[k] = C4 ? z[k] : pk_sub_u16(z[k], kOne + (c2[k] << 4));
+    // key word: sample m's class at bits 2m (pairs k: low half -> 4k, high half -> 4k + 2)
+    const uint32_t X = cp[0] | (cp[1] << 4) | (cp[2] << 8) | (cp[3] << 12);
+    const uint32_t Y = cp[4] | (cp[5] << 4) | (cp[6] << 8) | (cp[7] << 12);
+    const uint32_t Xn = (X & 0x3333u) | ((X >> 14) & 0xCCCCu), Yn = (Y & 0x3333u) | ((Y >> 14) & 0xCCCCu);
+    const uint32_t kw = Xn | (Yn << 16);
+    // places: step fills + the classes of the lanes below (one packed scan) + ranks within the lane
     const uint32_t lo = kw & 0x55555555u, hi = (kw >> 1) & 0x55555555u;
-    const uint32_t n1 = (uint32_t)__builtin_popcount(lo & ~hi), n2 = (uint32_t)__builtin_popcount(hi & ~lo);
-    const uint32_t n3 = (uint32_t)__builtin_popcount(lo & hi);
-    const uint32_t p12 = n1 | (n2 << 16);
-    const uint32_t i12 = wave_incl_sum(p12), i3 = wave_incl_sum(n3);
-    const uint32_t t12 = readlane_u32(i12, 63), t3 = readlane_u32(i3, 63);
-    const uint32_t e12 = i12 - p12;
-    uint32_t qS = fS + (e12 & 0xFFFFu), qM = fM + (e12 >> 16), qL = fL + (i3 - n3);
-    // one LDS byte per sample: the S or M window slot of its class (classes 0 and 3: a per-lane
-    // discard slot in the S window)
+    const uint32_t m1 = lo & ~hi, m2 = hi & ~lo, m3 = lo & hi;
+    const uint32_t pc = (uint32_t)__builtin_popcount(m1) | ((uint32_t)__builtin_popcount(m2) << 11) |
+                        ((uint32_t)__builtin_popcount(m3) << 22);
+    const uint32_t inc = wave_incl_sum(pc);
+    const uint32_t tot = readlane_u32(inc, 63);
+    const uint32_t exc = inc - pc;
     uint8_t* const wb = reinterpret_cast<uint8_t*>(&W);
     constexpr uint32_t offS = (uint32_t)__builtin_offsetof(SplitLds, S), offM = (uint32_t)__builtin_offsetof(SplitLds, M);
-    const uint32_t dS = offS + kDummy + 4u * lane;
+    const uint32_t baseS = offS + fS + (exc & 0x7FFu), baseM = offM + fM + ((exc >> 11) & 0x7FFu);
+    const uint32_t dS = offS + kDummy + 4u * lane;  // classes 0 and 3: a per-lane discard slot
 #pragma unroll
     for (int m = 0; m < 16; m++) {
-        const uint32_t c = (kw >> (2 * m)) & 3u;
-        const uint32_t at = (c == 1) ? offS + qS : ((c == 2) ? offM + qM : dS);
-        wb[at] = (uint8_t)(v[m] - ((c == 1) ? ClassOffsets<C4>::o1 : ClassOffsets<C4>::o2));
-        qS += (c == 1);
-        qM += (c == 2);
+        // class 1: S window at its rank among the lane's class-1 samples; class 2: M likewise;
+        // classes 0 and 3: the discard slot (empty mask, rank 0)
+        const uint32_t below = (1u << (2 * m)) - 1u;
+        const bool isS = (m1 >> (2 * m)) & 1u, isM = (m2 >> (2 * m)) & 1u;
+        const uint32_t msk = isS ? m1 : (isM ? m2 : 0u);
+        const uint32_t base = isS ? baseS : (isM ? baseM : dS);
+        const uint32_t at = base + (uint32_t)__builtin_popcount(msk & below);
+        wb[at] = (uint8_t)(val[m >> 1] >> (16 * (m & 1)));
     }
-    if (t3) {
+    // field 3 has 10 bits: a step of 1024 class-3 samples wraps the inclusive total (the exclusive
+    // prefixes stay exact), so its total is rebuilt from the last lane
+    const uint32_t t3 = (readlane_u32(exc, 63) >> 22) + (readlane_u32(pc, 63) >> 22);
+    if (t3) {  // class 3 is rare: each lane walks its own class-3 samples, values from an LDS stash
+        if (m3) {
 #pragma unroll
-        for (int m = 0; m < 16; m++) {
-            const uint32_t c = (kw >> (2 * m)) & 3u;
-            if (c == 3) {
-                const uint32_t w = v[m] - ClassOffsets<C4>::o3;
+            for (int k = 0; k < 8; k++) W.Z[8 * lane + k] = z[k];
+            uint32_t qL = fL + (exc >> 22);
+            const uint16_t* zs = reinterpret_cast<const uint16_t*>(W.Z) + 16 * lane;
+            for (uint32_t mm = m3; mm; mm &= mm - 1u) {
+                const uint32_t w = (uint32_t)zs[__builtin_ctz(mm) >> 1] - CO::o3;
                 W.L[qL] = (uint8_t)w;
                 W.H[qL] = (uint8_t)(w >> 8);
                 qL++;
             }
         }
     }
-    fS += t12 & 0xFFFFu;
-    fM += t12 >> 16;
+    fS += tot & 0x7FFu;
+    fM += (tot >> 11) & 0x7FFu;
     fL += t3;
     return kw;
 }
