@@ -286,10 +286,11 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
 // Returns 0 ok, 1 out-of-bounds; *consumed = one past the last Lhigh byte.
 // ---------------------------------------------------------------------------------------------
 struct MergeLds {
-    alignas(16) uint8_t S[528];   // 513 bytes of nibbles + alignment
-    alignas(16) uint8_t M[1040];  // 1024 + alignment
-    alignas(16) uint8_t L[1040];
-    alignas(16) uint8_t H[1040];
+    // one step's S, M and class-3 values as 16-bit entries with their class offsets added, back to
+    // back: S (one nibble per entry) from a 16-byte aligned stream byte, then M likewise, then L | H << 8.
+    // A step has at most 1024 of them together, plus the alignment slack of two windows.
+    alignas(16) uint16_t V[1024 + 64 + 32 + 32];
+    uint16_t zero[2];  // what a class-0 sample reads
 };
 
 // stage bytes [a, a + len) of `in` (len <= cap - 15) into W; returns the window's first address
@@ -301,46 +302,81 @@ __device__ __forceinline__ uint64_t stage_bytes(uint8_t* W, const uint8_t* in, u
     return a0;
 }
 
-// Merge step over 1024 samples: lane l decodes the 16 consecutive samples t + 16l .. t + 16l + 15,
-// whose 16 keys are its own key word.  Its places in the S / M / L streams are the step's fills
-// plus the class counts of the lanes below it (one packed DPP scan), so each lane walks its 16
-// samples alone: one LDS byte read per stream and sample, a running 16-bit sum, and a second scan
-// carries the sum across lanes.  Outputs leave as two 16-byte stores per lane.
-template <bool Full, bool C4 = false>
-__device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, bool any3, uint32_t qS, uint32_t qM, uint32_t qL,
-                                           uint32_t dLH, uint32_t& carry, int16_t* __restrict__ out, uint32_t t,
-                                           uint32_t n)
+// 16 bytes of nibbles -> 32 entries (low nibble first) + add, written at d
+__device__ __forceinline__ void put_nibbles16(uint16_t* d, const uint4& v, uint32_t add2)
 {
-    const uint32_t lane = (uint32_t)lane_id();
-    uint32_t acc = 0;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[16];
 #pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t y = __builtin_amdgcn_perm(0u, w[j], 0x0C000C00u + 0x00010001u * (uint32_t)k);  // byte k twice
+            o[4 * j + k] = ((y & 0xFu) | ((y >> 4) & 0x000F0000u)) + add2;
+        }
+    uint4* q = (uint4*)d;
+    q[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    q[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    q[2] = make_uint4(o[8], o[9], o[10], o[11]);
+    q[3] = make_uint4(o[12], o[13], o[14], o[15]);
+}
+// 16 bytes -> 16 entries + add, written at d
+__device__ __forceinline__ void put_bytes16(uint16_t* d, const uint4& v, uint32_t add2)
+{
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[8];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        o[2 * j] = __builtin_amdgcn_perm(0u, w[j], 0x0C010C00u) + add2;
+        o[2 * j + 1] = __builtin_amdgcn_perm(0u, w[j], 0x0C030C02u) + add2;
+    }
+    uint4* q = (uint4*)d;
+    q[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    q[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// Merge step over 1024 samples: lane l decodes the 16 consecutive samples t + 16l .. t + 16l + 15,
+// whose 16 keys are its own key word.  Every class has a staged 16-bit window with its offset
+// already added (class 0 reads a zero), and the lane's places in them are the step's fills plus
+// the class counts of the lanes below it (one packed DPP scan); so a sample is one LDS read at its
+// class's running place, a running 16-bit sum, and a second scan carries the sum across lanes.
+// Outputs leave as two 16-byte stores per lane.
+__device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, uint32_t pS, uint32_t pM, uint32_t pL,
+                                           uint32_t& carry, int16_t* __restrict__ out, uint32_t t, uint32_t n, bool full)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(&W);
+    constexpr uint32_t pZ = (uint32_t)__builtin_offsetof(MergeLds, zero);
+    uint32_t acc = 0;
+    uint32_t w[8];  // running sums, two 16-bit samples per word
+#pragma unroll
     for (int m = 0; m < 16; m++) {
-        const uint32_t c = (kw >> (2 * m)) & 3u;
-        const uint32_t sb = ((uint32_t)W.S[qS >> 1] >> (4u * (qS & 1u))) & 15u;
-        const uint32_t mb = W.M[qM];
-        uint32_t v = (c == 1) ? sb + ClassOffsets<C4>::o1 : ((c == 2) ? mb + ClassOffsets<C4>::o2 : 0u);
-        if (any3 && c == 3) v = (((uint32_t)W.H[qL + dLH] << 8) | (uint32_t)W.L[qL]) + ClassOffsets<C4>::o3;
-        qS += (c == 1);
-        qM += (c == 2);
-        qL += (c == 3);
+        // the class bits as all-ones / all-zero masks: a two-level bit-select picks the place
+        const uint32_t b0 = (uint32_t)(((int32_t)(kw << (31 - 2 * m))) >> 31);
+        const uint32_t b1 = (uint32_t)(((int32_t)(kw << (30 - 2 * m))) >> 31);
+        const uint32_t lo = (pS & b0) | (pZ & ~b0), hi = (pL & b0) | (pM & ~b0);
+        const uint32_t at = (hi & b1) | (lo & ~b1);
+        const uint32_t v = *reinterpret_cast<const uint16_t*>(wb + at);
+        pS += b0 & ~b1 & 2u;
+        pM += b1 & ~b0 & 2u;
+        pL += b0 & b1 & 2u;
         acc += (uint32_t)zz_dec16((uint16_t)v);
-        o[m] = acc;
+        if (m & 1) w[m >> 1] |= acc << 16;
+        else w[m >> 1] = acc & 0xFFFFu;
+        if (m % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // at most 4 places read ahead (VGPRs)
     }
     const uint32_t incl = wave_incl_sum(acc);
     const uint32_t base = carry + incl - acc;
     carry += readlane_u32(incl, 63);
-    uint32_t w[8];
+    const pgn_u16x2 base2 = as_u16x2((base & 0xFFFFu) * 0x00010001u);
 #pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = ((o[2 * k] + base) & 0xFFFFu) | ((o[2 * k + 1] + base) << 16);
+    for (int k = 0; k < 8; k++) w[k] = as_u32(as_u16x2(w[k]) + base2);
     int16_t* dst = out + t + 16u * lane;
-    if (Full) {
+    if (full) {
         gst<uint4>(dst, make_uint4(w[0], w[1], w[2], w[3]));
         gst<uint4>(dst + 8, make_uint4(w[4], w[5], w[6], w[7]));
     } else {
-#pragma unroll
-        for (int m = 0; m < 16; m++)
-            if (t + 16u * lane + (uint32_t)m < n) gst<uint16_t>(dst + m, (uint16_t)(w[m >> 1] >> (16 * (m & 1))));
+        for (uint32_t m = 0; m < 16 && t + 16u * lane + m < n; m++) gst<uint16_t>(dst + m, (uint16_t)(w[m >> 1] >> (16 * (m & 1))));
     }
 }
 
@@ -354,6 +390,7 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
     const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
     uint64_t sN = 0, mN = 0, lN = 0;  // nibbles / bytes consumed so far (wave-uniform)
     uint32_t carry = 0;
+    if (lane == 0) W.zero[0] = 0;
     for (uint32_t t = 0; t < n; t += kSplitStep) {
         const bool full = t + kSplitStep <= n;
         const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
@@ -379,22 +416,39 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
         const uint32_t ns = t12 & 0xFFFFu, nm = t12 >> 16, nl = readlane_u32(i3, 63);
         if (ps + ((sN + ns + 1) >> 1) > total || pm + mN + nm > total || pl + lN + nl > total || ph + lN + nl > total)
             return 1;
-        const uint64_t wS = stage_bytes(W.S, in, ps + (sN >> 1), (uint32_t)(((sN + ns + 1) >> 1) - (sN >> 1)));
-        const uint64_t wM = stage_bytes(W.M, in, pm + mN, nm);
-        uint64_t wL = 0, wH = 0;
-        if (nl) {
-            wL = stage_bytes(W.L, in, pl + lN, nl);
-            wH = stage_bytes(W.H, in, ph + lN, nl);
+        // stage the step's values: S blocks, then M blocks, then the class-3 values, into one window;
+        // the first 64 blocks of each and 64 class-3 values are loaded together
+        const uint64_t aS = ps + (sN >> 1), aS0 = aS & ~(uint64_t)15;
+        const uint32_t nbS = (uint32_t)((ps + ((sN + ns + 1) >> 1) - aS0 + 15) >> 4);
+        const uint64_t aM = pm + mN, aM0 = aM & ~(uint64_t)15;
+        const uint32_t nbM = (uint32_t)((aM + nm - aM0 + 15) >> 4);
+        const uint32_t eM = 32u * nbS, eL = eM + 16u * nbM;  // entry offsets of the M and class-3 windows
+        {
+            constexpr uint32_t add1 = ClassOffsets<C4>::o1 * 0x00010001u, add2 = ClassOffsets<C4>::o2 * 0x00010001u;
+            uint4 vS = make_uint4(0, 0, 0, 0), vM = vS;
+            uint32_t lb = 0, hb = 0;
+            if (lane < nbS) vS = gld<uint4>(in + aS0 + 16u * lane);
+            if (lane < nbM) vM = gld<uint4>(in + aM0 + 16u * lane);
+            if (lane < nl) {
+                lb = gb(in + pl + lN + lane);
+                hb = gb(in + ph + lN + lane);
+            }
+            if (lane < nbS) put_nibbles16(W.V + 32u * lane, vS, add1);
+            if (lane < nbM) put_bytes16(W.V + eM + 16u * lane, vM, add2);
+            if (lane < nl) W.V[eL + lane] = (uint16_t)((lb | (hb << 8)) + ClassOffsets<C4>::o3);
+            for (uint32_t b = lane + 64; b < nbS; b += 64) put_nibbles16(W.V + 32u * b, gld<uint4>(in + aS0 + 16u * b), add1);
+            for (uint32_t b = lane + 64; b < nbM; b += 64) put_bytes16(W.V + eM + 16u * b, gld<uint4>(in + aM0 + 16u * b), add2);
+            for (uint32_t i = lane + 64; i < nl; i += 64)
+                W.V[eL + i] = (uint16_t)(((uint32_t)gb(in + pl + lN + i) | ((uint32_t)gb(in + ph + lN + i) << 8)) + ClassOffsets<C4>::o3);
         }
         lds_sync();
-        // window-relative places: S in nibbles from the window start, M/L in bytes
+        // LDS byte places of my first value of each class
+        constexpr uint32_t offV = (uint32_t)__builtin_offsetof(MergeLds, V);
         const uint32_t e12 = i12 - p12;
-        const uint32_t qS = (uint32_t)(2 * (ps - wS) + sN) + (e12 & 0xFFFFu);
-        const uint32_t qM = (uint32_t)(pm + mN - wM) + (e12 >> 16);
-        const uint32_t qL = (uint32_t)(pl + lN - wL) + (i3 - n3);
-        const uint32_t dLH = (uint32_t)((ph - wH) - (pl - wL));  // H window offset relative to L's
-        if (full) merge_step<true, C4>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
-        else merge_step<false, C4>(W, kw, nl != 0, qS, qM, qL, dLH, carry, out, t, n);
+        const uint32_t pS = offV + 2u * ((uint32_t)(2 * (aS - aS0) + (sN & 1)) + (e12 & 0xFFFFu));
+        const uint32_t pM = offV + 2u * (eM + (uint32_t)(aM - aM0) + (e12 >> 16));
+        const uint32_t pL = offV + 2u * (eL + (i3 - n3));
+        merge_step(W, kw, pS, pM, pL, carry, out, t, n, full);
         sN += ns;
         mN += nm;
         lN += nl;
