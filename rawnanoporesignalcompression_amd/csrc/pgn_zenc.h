@@ -8,6 +8,9 @@
 //   * Huffman bit packing (prefix sum of code lengths, LDS window, byte flush).
 // Serial stages (tree build, weight FSE, sequence FSE) run on lane 0 with the shared zstd1_* code.
 #pragma once
+#ifndef PGN_AB_SKIP
+#define PGN_AB_SKIP 0  // diagnostic builds (tools/ab_skip.sh): 1 no zstd stage, 2 search only, 3 no Huffman, 4 no bit packing
+#endif
 #include "pgn_c5.h"
 #include "pgn_wave.h"
 #include "zstd1_model.h"
@@ -1332,6 +1335,9 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     const uint32_t largest = wave_max(myLargest);
     wave_sync();
     P.mark(3);
+#if PGN_AB_SKIP == 3
+    { size_t r = write_raw_literals_wave(dst, lit, n); return ret(r, false); }
+#endif
     if (largest == n) {  // one symbol: RLE literals
         size_t fl = z1::raw_lit_header_size(n);
         if (lane == 0) {
@@ -1364,28 +1370,50 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     }
     wave_sync();
     {
-        // one compare per pair on the key count << 8 | (255 - symbol): t ranks before s iff
-        // count_t > count_s, or equal counts and t < s; four counts per round of loads
-        uint32_t rank[4] = {0, 0, 0, 0}, key[4];
+        // HUF_sort order = descending key count << 8 | (255 - symbol) (stable by symbol): a bitonic
+        // sort of the 256 keys, four per lane (element e = lane + 64q), ascending on ~key so that
+        // absent symbols (key 0) come last; sorted element e is then the leaf of rank e
+        uint32_t a[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) key[q] = (c[q] << 8) | (255u - ((uint32_t)lane + 64u * (uint32_t)q));
-        const uint32_t T = maxSym + 1;
-        for (uint32_t t0 = 0; t0 < T; t0 += 4) {
-            uint32_t kt[4];
+        for (int q = 0; q < 4; q++) {
+            const uint32_t sy = (uint32_t)lane + 64u * (uint32_t)q;
+            a[q] = (sy <= maxSym) ? ~((c[q] << 8) | (255u - sy)) : 0xFFFFFFFFu;
+        }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t t = t0 + (uint32_t)u;
-                kt[u] = (t < T) ? ((L.count[t] << 8) | (255u - t)) : 0u;
+        for (uint32_t k = 2; k <= 256; k <<= 1) {
+#pragma unroll
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                if (j >= 64) {  // partner in another register of the same lane
+                    const uint32_t qj = j >> 6;
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; q++) {
+                        if (q & qj) continue;
+                        const uint32_t q2 = q | qj;
+                        const uint32_t mn = a[q] < a[q2] ? a[q] : a[q2], mx = a[q] < a[q2] ? a[q2] : a[q];
+                        const bool asc = ((64u * q) & k) == 0;
+                        a[q] = asc ? mn : mx;
+                        a[q2] = asc ? mx : mn;
+                    }
+                } else {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; q++) {
+                        const uint32_t b = (uint32_t)__shfl_xor((int)a[q], (int)j, 64);
+                        const uint32_t mn = a[q] < b ? a[q] : b, mx = a[q] < b ? b : a[q];
+                        const uint32_t e = (uint32_t)lane + 64u * q;
+                        const bool lower = (e & j) == 0, asc = (e & k) == 0;
+                        a[q] = (lower == asc) ? mn : mx;
+                    }
+                }
             }
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) rank[q] += kt[u] > key[q] ? 1u : 0u;
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            uint32_t s = (uint32_t)lane + 64u * (uint32_t)q;
-            if (s <= maxSym) { L.nodes[1 + rank[q]].count = c[q]; L.nodes[1 + rank[q]].byte = (uint8_t)s; }
+            const uint32_t r = (uint32_t)lane + 64u * (uint32_t)q;
+            if (r <= maxSym) {
+                const uint32_t key = ~a[q];
+                L.nodes[1 + r].count = key >> 8;
+                L.nodes[1 + r].byte = (uint8_t)(255u - (key & 0xFFu));
+            }
         }
     }
     wave_sync();
@@ -1456,7 +1484,9 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     for (int k = 0; k < nseg; k++) {
         uint32_t a = segSize * (uint32_t)k;
         uint32_t e = (k == nseg - 1) ? n : a + segSize;
+#if PGN_AB_SKIP != 4
         huf_encode_segment_wave(op, lit + a, e - a, bits[k]);
+#endif
         P.count(7, (e - a + 1023) / 1024);
         op += bytes[k];
     }
@@ -1515,13 +1545,20 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         uint8_t* bdst = dst + o;
         uint32_t cSize = 0;  // 0: raw block, 1: RLE block, else compressed body size
         size_t seqSize = 0;
+#if PGN_AB_SKIP == 1
+        if (false) {
+#else
         if (bs >= 7) {
+#endif
             const SearchOut so = fast_search_wave(src, start, start + bs, p.hashLog, p.mls, S.ht, tag, S.seqs, rep0, rep1);
             const uint32_t nbSeq = uni(so.nbSeq), lastLL = uni(so.lastLL);
             P.mark(1);
             P.count(0, uni(so.rounds));
             P.count(1, nbSeq);
             P.count(13);
+#if PGN_AB_SKIP == 2
+            if (uni(so.nbSeq) < 0x7FFFFFFFu) goto raw_block;
+#endif
             const uint8_t* lit = src + start;
             uint32_t nLit = bs;
             if (nbSeq > 0) {
@@ -1570,6 +1607,9 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
                 }
             }
         }
+#if PGN_AB_SKIP == 2
+    raw_block:
+#endif
         wave_sync();
         size_t bsz;
         if (cSize == 0) {

@@ -19,9 +19,13 @@ S = 100000
 c = PGNanoCodec(0)
 samples, offs, cnt = c.synth_reads(R, S, seed=42)
 enc = c.compress_batch(samples, offs, cnt)
-out, so, st = c.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
-torch.cuda.synchronize()
-print("encode ms", c.last_encode_ms(), "decode ms", c.last_decode_ms(), "ok", bool(torch.equal(out, samples)))
+if os.environ.get("PGN_ENCODE_ONLY"):  # diagnostic builds whose blobs are not decodable
+    torch.cuda.synchronize()
+    print("encode ms", c.last_encode_ms())
+else:
+    out, so, st = c.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
+    torch.cuda.synchronize()
+    print("encode ms", c.last_encode_ms(), "decode ms", c.last_decode_ms(), "ok", bool(torch.equal(out, samples)))
 buf = np.zeros(64, np.uint64)
 c._lib.pgn_debug_phase_cycles(c._h, buf.ctypes.data, 64)
 for name, lab, arr in (("encode", ENC, buf[:16]), ("decode", DEC, buf[16:])):
