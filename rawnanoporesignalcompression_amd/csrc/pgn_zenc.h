@@ -451,26 +451,29 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
         const uint32_t incl = wave_incl_sum(myBits);
         const uint32_t stepBits = readlane_u32(incl, 63);
         uint32_t pos = bitBase + (incl - myBits) - winLo;  // window-relative bit position
+        // a group (<= 44 bits) at bit pos touches words w .. w + 2: three unconditional ORs (of zero
+        // where it does not reach), no branches
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const uint32_t n = gnb[g];
-            if (n) {
-                const uint32_t w = pos >> 5, sh = pos & 31;
-                const uint64_t lo = grp[g] << sh;
-                atomicOr(&win[w], (uint32_t)lo);
-                if (sh + n > 32) atomicOr(&win[w + 1], (uint32_t)(lo >> 32));
-                if (sh + n > 64) atomicOr(&win[w + 2], (uint32_t)(grp[g] >> (64 - sh)));
-            }
-            pos += n;
+            const uint32_t w = pos >> 5, sh = pos & 31;
+            const uint64_t lo = grp[g] << sh;
+            atomicOr(&win[w], (uint32_t)lo);
+            atomicOr(&win[w + 1], (uint32_t)(lo >> 32));
+            atomicOr(&win[w + 2], (uint32_t)((grp[g] >> 32) >> (32 - sh)));
+            pos += gnb[g];
         }
         lds_sync();
         const uint32_t endRel = bitBase + stepBits - winLo;
         const uint32_t complete = endRel >> 5;
         uint8_t* o = out + (winLo >> 3);
-        for (uint32_t w = lane; w < complete; w += 64) gst<uint32_t>(o + 4 * w, win[w]);
+        // complete words leave and are cleared in one pass; the partial word moves to the front
         const uint32_t carry = win[complete];
-        lds_sync();
-        for (uint32_t w = lane; w <= complete; w += 64) win[w] = (w == 0) ? carry : 0u;
+        for (uint32_t w = lane; w <= complete; w += 64) {
+            const uint32_t v = win[w];
+            if (w < complete) gst<uint32_t>(o + 4 * w, v);
+            win[w] = 0u;
+        }
+        if (lane == 0) win[0] = carry;
         lds_sync();
         winLo += complete * 32;
         bitBase += stepBits;
