@@ -168,6 +168,7 @@ __device__ inline uint32_t wave_back_count(const uint8_t* src, uint32_t a, uint3
 // fast_search_serial); rep0 / rep1 are the confirmed repeat offsets on entry.
 struct SearchOut {
     uint32_t nbSeq, lastLL, rep0, rep1, rounds;
+    uint32_t candIters;  // profile builds: wave iterations of the same-slot loops
 };
 __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ src, uint32_t start, uint32_t end, unsigned hlog,
                                                    unsigned mls, uint32_t* __restrict__ ht, uint32_t tag,
@@ -191,7 +192,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     uint32_t off1 = rep0, off2 = rep1, offSaved = 0;
     if (off2 > (uint32_t)ip0) { offSaved = off2; off2 = 0; }
     if (off1 > (uint32_t)ip0) { offSaved = off1; off1 = 0; }
-    uint32_t nbSeq = 0, rounds = 0;
+    uint32_t nbSeq = 0, rounds = 0, candIters = 0;
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
     lds_sync();
@@ -259,7 +260,13 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         // value each slot holds at my visit: the latest earlier writer in this round, else the table
         uint32_t m0 = ((t0 >> kTagShift) == tag) ? (t0 & ((1u << kTagShift) - 1u)) : 0u;
         uint32_t m1 = ((t1 >> kTagShift) == tag) ? (t1 & ((1u << kTagShift) - 1u)) : 0u;
+#ifdef PGN_PROFILE
+        uint32_t myIt = 0;
+#endif
         for (uint64_t cand = M0 & below; cand;) {
+#ifdef PGN_PROFILE
+            myIt++;
+#endif
             const int jj = 63 - __builtin_clzll(cand);
             const uint32_t pj = L.vpk[jj];
             if (L.vh1[jj] == h0) { m0 = pj + 2; break; }
@@ -267,6 +274,9 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             cand &= ~(1ull << jj);
         }
         for (uint64_t cand = M1 & below; cand;) {
+#ifdef PGN_PROFILE
+            myIt++;
+#endif
             const int jj = 63 - __builtin_clzll(cand);
             const uint32_t pj = L.vpk[jj];
             if (L.vh1[jj] == h1) { m1 = pj + 2; break; }
@@ -279,6 +289,9 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             c0 = (m0 > 1) && (ld32u(src + m0 - 1) == (uint32_t)v8);
             c1 = (m1 > 1) && (ld32u(src + m1 - 1) == (uint32_t)(v8 >> 8));
         }
+#ifdef PGN_PROFILE
+        candIters += wave_max(myIt);
+#endif
         const uint64_t hits = ballot(rep || c0 || c1);
         const uint64_t vmask = ballot(valid);
         const int f = hits ? __builtin_ctzll(hits) : 64;
@@ -381,6 +394,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     r.rep0 = off1 ? off1 : offSaved;
     r.rep1 = off2 ? off2 : offSaved;
     r.rounds = rounds;
+    r.candIters = candIters;
     return r;
 }
 
@@ -1557,6 +1571,7 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
             const uint32_t nbSeq = uni(so.nbSeq), lastLL = uni(so.lastLL);
             P.mark(1);
             P.count(0, uni(so.rounds));
+            P.count(14, uni(so.candIters));
             P.count(1, nbSeq);
             P.count(13);
 #if PGN_AB_SKIP == 2

@@ -44,7 +44,7 @@ for i, l in enumerate(DCNT):
         print(f"   {l:24s} {buf[48 + i] / R:12.2f}")
 ECNT = ["search rounds", "sequences found", "tree builds", "tree merge rounds", "depth iters", "writeCTable",
         "ctable symbols", "huf encode steps", "hist iters", "split steps", "seq sections", "seqs encoded",
-        "frames", "blocks", "-", "-"]
+        "frames", "blocks", "search same-slot iters", "-"]
 print("encode counters per chunk:")
 for i, l in enumerate(ECNT):
     if buf[32 + i]:
