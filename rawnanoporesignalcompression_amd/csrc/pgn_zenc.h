@@ -35,6 +35,7 @@ struct alignas(16) EncLds {
         struct {  // match search: hash-slot filter of the current round (bit per lane), the round's visits
             uint64_t filt[kFiltSlots];
             uint32_t vh0[64], vh1[64], vpk[64];
+            uint32_t vd0[64], vd1[64];  // the 4 bytes at the round's visits pk and pk + 1
         };
         struct {  // literals; members grouped by lifetime so that each phase's scratch overlays the last
             uint32_t hist2[2][256];  // per-segment histograms, two 16-bit counts per word (histogram -> stream sizes)
@@ -90,7 +91,7 @@ __device__ __forceinline__ uint32_t seg_count(const EncLds& L, int k, int s)
 static __shared__ EncLds sEnc;
 
 struct EncScratch {
-    uint32_t* ht;        // 2^15 tagged hash-table entries (tag << kTagShift | index)
+    uint64_t* ht;        // 2^15 hash-table entries: tag << kTagShift | index, and the 4 bytes at that position
     z1::Seq* seqs;       // <= stream/4 + 2 sequences
     uint8_t* codes;      // 3 * (stream/4 + 2)
     uint8_t* lit;        // gathered literals (stream bytes)
@@ -134,6 +135,12 @@ constexpr uint32_t kTagShift = 20;
 constexpr uint32_t kTagEpochs = 1u << (32 - kTagShift);
 static_assert(z1::kMaxFrameSrc + 2 < (1u << kTagShift), "index field");
 __device__ inline uint32_t tagged(uint32_t tag, uint32_t idx) { return (tag << kTagShift) | idx; }
+// a table entry: the tagged index (position + 1) and MEM_read32 of the position, so that a
+// candidate is tested without reading the stream again
+__device__ inline uint64_t ht_entry(uint32_t tag, uint32_t idx, uint32_t bytes)
+{
+    return (uint64_t)tagged(tag, idx) | ((uint64_t)bytes << 32);
+}
 
 // ZSTD_hashPtr (mls 5 / 6 / 7) over 8 global bytes
 __device__ __forceinline__ uint32_t hash_g(const uint8_t* p, unsigned hlog, unsigned mls)
@@ -171,7 +178,7 @@ struct SearchOut {
     uint32_t candIters;  // profile builds: wave iterations of the same-slot loops
 };
 __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ src, uint32_t start, uint32_t end, unsigned hlog,
-                                                   unsigned mls, uint32_t* __restrict__ ht, uint32_t tag,
+                                                   unsigned mls, uint64_t* __restrict__ ht, uint32_t tag,
                                                    z1::Seq* __restrict__ seqs, uint32_t rep0, uint32_t rep1)
 {
     EncLds& L = sEnc;
@@ -227,19 +234,22 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         }
         havePk = false;
         const bool valid = (pk + 1 < ilimit);
-        uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu, t0 = 0, t1 = 0;
+        uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu;
+        uint64_t t0 = 0, t1 = 0;
         uint64_t M0 = 0, M1 = 0;
         if (valid) {
             h0 = z1::hash_word(v8, hlog, mls);
             h1 = z1::hash_word(v8 >> 8, hlog, mls);
-            t0 = gld<uint32_t>(ht + h0);
-            t1 = gld<uint32_t>(ht + h1);
+            t0 = gld<uint64_t>(ht + h0);
+            t1 = gld<uint64_t>(ht + h1);
             atomicOr((unsigned long long*)&L.filt[h0 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
             atomicOr((unsigned long long*)&L.filt[h1 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
         }
         L.vh0[lane] = h0;
         L.vh1[lane] = h1;
         L.vpk[lane] = (uint32_t)pk;
+        L.vd0[lane] = (uint32_t)v8;
+        L.vd1[lane] = (uint32_t)(v8 >> 8);
         // the next round's visits and their bytes, assuming this one finds no match (overlaps the
         // table reads)
         int32_t pkN, pNextN;
@@ -258,8 +268,9 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             L.filt[h1 & (kFiltSlots - 1)] = 0;
         }
         // value each slot holds at my visit: the latest earlier writer in this round, else the table
-        uint32_t m0 = ((t0 >> kTagShift) == tag) ? (t0 & ((1u << kTagShift) - 1u)) : 0u;
-        uint32_t m1 = ((t1 >> kTagShift) == tag) ? (t1 & ((1u << kTagShift) - 1u)) : 0u;
+        uint32_t m0 = (((uint32_t)t0 >> kTagShift) == tag) ? ((uint32_t)t0 & ((1u << kTagShift) - 1u)) : 0u;
+        uint32_t m1 = (((uint32_t)t1 >> kTagShift) == tag) ? ((uint32_t)t1 & ((1u << kTagShift) - 1u)) : 0u;
+        uint32_t d0 = (uint32_t)(t0 >> 32), d1 = (uint32_t)(t1 >> 32);
 #ifdef PGN_PROFILE
         uint32_t myIt = 0;
 #endif
@@ -269,8 +280,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
 #endif
             const int jj = 63 - __builtin_clzll(cand);
             const uint32_t pj = L.vpk[jj];
-            if (L.vh1[jj] == h0) { m0 = pj + 2; break; }
-            if (L.vh0[jj] == h0) { m0 = pj + 1; break; }
+            if (L.vh1[jj] == h0) { m0 = pj + 2; d0 = L.vd1[jj]; break; }
+            if (L.vh0[jj] == h0) { m0 = pj + 1; d0 = L.vd0[jj]; break; }
             cand &= ~(1ull << jj);
         }
         for (uint64_t cand = M1 & below; cand;) {
@@ -279,15 +290,15 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
 #endif
             const int jj = 63 - __builtin_clzll(cand);
             const uint32_t pj = L.vpk[jj];
-            if (L.vh1[jj] == h1) { m1 = pj + 2; break; }
-            if (L.vh0[jj] == h1) { m1 = pj + 1; break; }
+            if (L.vh1[jj] == h1) { m1 = pj + 2; d1 = L.vd1[jj]; break; }
+            if (L.vh0[jj] == h1) { m1 = pj + 1; d1 = L.vd0[jj]; break; }
             cand &= ~(1ull << jj);
         }
         bool rep = false, c0 = false, c1 = false;
         if (valid) {
             rep = (off1 > 0) && (repw == (uint32_t)(v8 >> 16));
-            c0 = (m0 > 1) && (ld32u(src + m0 - 1) == (uint32_t)v8);
-            c1 = (m1 > 1) && (ld32u(src + m1 - 1) == (uint32_t)(v8 >> 8));
+            c0 = (m0 > 1) && (d0 == (uint32_t)v8);
+            c1 = (m1 > 1) && (d1 == (uint32_t)(v8 >> 8));
         }
 #ifdef PGN_PROFILE
         candIters += wave_max(myIt);
@@ -310,8 +321,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
                 if (L.vh0[jj] == h1 || L.vh1[jj] == h1) w1 = false;
                 cand &= cand - 1;
             }
-            if (w0) gst<uint32_t>(ht + h0, tagged(tag, (uint32_t)pk + 1));
-            if (w1) gst<uint32_t>(ht + h1, tagged(tag, (uint32_t)pk + 2));
+            if (w0) gst<uint64_t>(ht + h0, ht_entry(tag, (uint32_t)pk + 1, (uint32_t)v8));
+            if (w1) gst<uint64_t>(ht + h1, ht_entry(tag, (uint32_t)pk + 2, (uint32_t)(v8 >> 8)));
         }
         lds_sync();
         if (!hits) {
@@ -365,8 +376,9 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         anchor = ip0;
         if (ip0 <= ilimit) {
             if (lane == 0) {
-                gst<uint32_t>(ht + hash_g(src + cur0 + 1, hlog, mls), tagged(tag, cur0 + 2));
-                gst<uint32_t>(ht + hash_g(src + ip0 - 2, hlog, mls), tagged(tag, (uint32_t)(ip0 - 2) + 1));
+                const uint64_t wa = ld64u(src + cur0 + 1), wb = ld64u(src + ip0 - 2);
+                gst<uint64_t>(ht + z1::hash_word(wa, hlog, mls), ht_entry(tag, cur0 + 2, (uint32_t)wa));
+                gst<uint64_t>(ht + z1::hash_word(wb, hlog, mls), ht_entry(tag, (uint32_t)(ip0 - 2) + 1, (uint32_t)wb));
             }
             if (off2 > 0) {
                 while ((ip0 <= ilimit) && (ld32u(src + ip0) == ld32u(src + ip0 - (int32_t)off2))) {
@@ -375,7 +387,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
                     off2 = off1;
                     off1 = t;
                     if (lane == 0) {
-                        gst<uint32_t>(ht + hash_g(src + ip0, hlog, mls), tagged(tag, (uint32_t)ip0 + 1));
+                        const uint64_t wr = ld64u(src + ip0);
+                        gst<uint64_t>(ht + z1::hash_word(wr, hlog, mls), ht_entry(tag, (uint32_t)ip0 + 1, (uint32_t)wr));
                         seqs[nbSeq].litLength = 0;
                         seqs[nbSeq].offset = 1;
                         seqs[nbSeq].mlBase = rLength - 3;
