@@ -33,7 +33,8 @@ typedef enum pgn_status {
     PGN_ERR_UNSUPPORTED = 9,      /* chunk larger than PGN_MAX_CHUNK_SAMPLES, or a stream above 512 KiB */
     PGN_ERR_INVALID_ARG = 10,
     PGN_ERR_HIP = 11,             /* HIP runtime failure (message in pgn_last_error) */
-    PGN_ERR_NO_DEVICE = 12
+    PGN_ERR_NO_DEVICE = 12,
+    PGN_ERR_IO = 13               /* file open/read/write failure (pgnano_pod5file.h) */
 } pgn_status;
 
 /* Largest chunk the GPU path encodes and decodes.  Every stream is one zstd frame of up to four

@@ -37,6 +37,9 @@ extern "C" {
 
 typedef struct pgn_pod5_batch pgn_pod5_batch;
 
+/* Detail of the last failure of a pgn_pod5_* call on this thread (HIP error, failing row). */
+const char *pgn_pod5_last_error(void);
+
 /* A batch object on `ctx` (which it does not own) for one codec and chunk size (0 = the writer's
  * default, at most PGN_MAX_CHUNK_SAMPLES).  It keeps its staging buffers between calls. */
 int pgn_pod5_batch_create(pgn_ctx *ctx, int codec, uint32_t chunk_size, pgn_pod5_batch **out);

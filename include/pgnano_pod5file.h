@@ -1,0 +1,123 @@
+/*
+ * pgnano_pod5file.h -- POD5 container I/O for the signal table, without Arrow (C ABI).
+ *
+ * A POD5 file is a "combined file" (pod5/docs/SPECIFICATION.md "Combined file Layout"):
+ *   <signature "\213POD\r\n\032\n"> <section marker, 16 bytes>
+ *   <embedded Arrow IPC file (padded to 8 bytes)> <section marker> ...
+ *   <"FOOTER\0\0"> <footer flatbuffer (padded to 8)> <int64 footer length> <section marker> <signature>
+ * The footer (pod5/c++/pod5_format/flatbuffers/footer.fbs) lists the embedded files: the signal
+ * table, the run-info table and the reads table (written in that order by file_writer.cpp:300-350,
+ * footer by internal/combined_file_utils.h:85-151, read back by combined_file_utils.h:188-279).
+ * The signal table (signal_table_schema.cpp:15-42) has three columns: read_id (minknow.uuid,
+ * fixed_size_binary(16)), signal (minknow.vbz or pgnano.signal over large_binary, or
+ * large_list<int16> uncompressed) and samples (uint32), in record batches of 100 rows
+ * (file_writer.h:23 DEFAULT_SIGNAL_TABLE_BATCH_SIZE).
+ *
+ * This header replaces the Arrow-based pieces of that path with a native reader and writer: the
+ * footer and the Arrow IPC file format (flatbuffer schema, record batch and footer messages) are
+ * parsed and written directly, so the signal column can be handed to the GPU codec without Arrow.
+ * The other embedded tables are not interpreted: a writer given a source file copies them byte for
+ * byte (what the reference's `copy` does to them when only the signal codec changes).
+ *
+ * pgn_pod5_transcode_file (GPU) is `copy in.pod5 out.pod5 --pgnano | --VBZ` for the signal table:
+ * the rows are decoded and re-encoded by batched launches (pgnano_pod5.h's codecs) and written with
+ * the source's row order, read ids, reads and run-info tables.
+ */
+#ifndef PGNANO_POD5FILE_H
+#define PGNANO_POD5FILE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "pgnano_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* footer.fbs ContentType */
+#define PGN_POD5_CONTENT_READS 0
+#define PGN_POD5_CONTENT_SIGNAL 1
+#define PGN_POD5_CONTENT_READ_ID_INDEX 2
+#define PGN_POD5_CONTENT_OTHER_INDEX 3
+#define PGN_POD5_CONTENT_RUN_INFO 4
+
+/* signal_table_utils.h:5 SignalType */
+#define PGN_POD5_SIGNAL_UNCOMPRESSED 0
+#define PGN_POD5_SIGNAL_VBZ 1
+#define PGN_POD5_SIGNAL_PGNANO 2
+
+/* file_writer.h:23 */
+#define PGN_POD5_DEFAULT_SIGNAL_BATCH_ROWS 100u
+
+typedef struct pgn_pod5_file pgn_pod5_file;
+
+/* Text of the last failure of a pgn_pod5_file_* / pgn_pod5_write_* call on this thread. */
+const char *pgn_pod5_file_error(void);
+
+/* Opens a combined POD5 file: checks both signatures, parses the footer and the signal table's
+ * schema and record-batch index (combined_file_utils.h:188-279, signal_table_schema.cpp:45-80).
+ * PGN_ERR_CORRUPT for a malformed file, PGN_ERR_UNSUPPORTED for body-compressed or null-bearing
+ * signal batches. */
+int pgn_pod5_file_open(const char *path, pgn_pod5_file **out);
+int pgn_pod5_file_close(pgn_pod5_file *f);
+
+/* Footer strings (valid while f is open). */
+const char *pgn_pod5_file_identifier(const pgn_pod5_file *f);
+const char *pgn_pod5_file_software(const pgn_pod5_file *f);
+const char *pgn_pod5_file_pod5_version(const pgn_pod5_file *f);
+
+/* The footer's embedded files, in footer order. */
+int pgn_pod5_file_embedded_count(const pgn_pod5_file *f);
+int pgn_pod5_file_embedded(const pgn_pod5_file *f, int index, int64_t *offset, int64_t *length, int *content_type);
+
+/* Signal table shape: rows, record batches, the signal type (PGN_POD5_SIGNAL_*), the bytes of the
+ * signal column's data (compressed bytes, or 2 x samples when uncompressed) and the sum of the
+ * samples column. */
+int pgn_pod5_signal_info(const pgn_pod5_file *f, uint64_t *rows, uint32_t *batches, int *signal_type,
+                         uint64_t *data_bytes, uint64_t *total_samples);
+
+/* Copies the signal table out, all batches in order (any pointer may be NULL to skip a column):
+ *   read_ids  16 x rows bytes;  samples  rows entries;
+ *   offsets   rows + 1 byte offsets into data (offsets[0] = 0);  data  data_bytes bytes
+ *   (little-endian int16 samples when the table is uncompressed). */
+int pgn_pod5_signal_read(const pgn_pod5_file *f, uint8_t *read_ids, uint32_t *samples, uint64_t *offsets,
+                         uint8_t *data);
+
+/* Writes a combined POD5 file whose signal table holds the given rows (row i: read_ids[16 i ..],
+ * samples[i], signal bytes data[offsets[i] .. offsets[i + 1])) as `signal_type`, in record batches
+ * of rows_per_batch rows (0 = 100).
+ * With `source` (may be NULL): the footer's file identifier, software and pod5 version and the
+ * signal table's schema metadata are the source's, and every embedded table of the source other
+ * than its signal table is copied byte for byte after the signal table, in footer order.
+ * Without: a signal-table-only file with a fresh file identifier, `software` (NULL =
+ * "rawnanoporesignalcompression_amd") and pod5 version "0.3.10".
+ * section_marker: 16 bytes, or NULL for a random one. */
+int pgn_pod5_write_file(const char *path, const pgn_pod5_file *source, int signal_type, uint64_t rows,
+                        const uint8_t *read_ids, const uint32_t *samples, const uint64_t *offsets, const uint8_t *data,
+                        uint32_t rows_per_batch, const char *software, const uint8_t *section_marker);
+
+typedef struct pgn_pod5_transcode_stats {
+    uint64_t rows;
+    uint64_t samples;
+    uint64_t in_bytes;   /* signal column data of the input */
+    uint64_t out_bytes;  /* signal column data written */
+    float decode_ms;     /* device time of the batched decode (0 when the input is uncompressed) */
+    float encode_ms;     /* device time of the batched encode (0 when the output is uncompressed) */
+} pgn_pod5_transcode_stats;
+
+/* `copy in.pod5 out.pod5 --pgnano | --VBZ` on the GPU for the signal table: every row of the input
+ * is decoded by one batched launch (its codec from the signal column's type; pgnano blobs with
+ * `pgnano_variant`, PGN_VARIANT_C5 for the reference's default build), re-encoded by one batched
+ * launch as `dst_signal_type` (PGN_POD5_SIGNAL_*), packed on the device, and written with
+ * pgn_pod5_write_file(source = the input).  Rows above PGN_MAX_CHUNK_SAMPLES samples fail with
+ * PGN_ERR_UNSUPPORTED; a row the codec refuses fails the call with its status (detail in
+ * pgn_pod5_last_error, pgnano_pod5.h). */
+int pgn_pod5_transcode_file(pgn_ctx *ctx, const char *in_path, const char *out_path, int dst_signal_type,
+                            int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PGNANO_POD5FILE_H */

@@ -25,6 +25,7 @@ PGN_ERR_UNSUPPORTED = 9
 PGN_ERR_INVALID_ARG = 10
 PGN_ERR_HIP = 11
 PGN_ERR_NO_DEVICE = 12
+PGN_ERR_IO = 13
 
 PGN_POD5_CODEC_VBZ = 100  # include/pgnano_pod5.h
 PGN_MAX_CHUNK_SAMPLES = 262144
@@ -75,6 +76,23 @@ SIGNATURES = [
     ("pgn_pod5_compress_reads", C.c_int, [_VP, C.c_uint32, _VP, _VP, C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
     ("pgn_pod5_decompress_rows", C.c_int, [_VP, C.c_uint32, _VP, _VP, _VP, _VP, _VP]),
+    ("pgn_pod5_last_error", C.c_char_p, []),
+    # include/pgnano_pod5file.h
+    ("pgn_pod5_file_error", C.c_char_p, []),
+    ("pgn_pod5_file_open", C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
+    ("pgn_pod5_file_close", C.c_int, [_VP]),
+    ("pgn_pod5_file_identifier", C.c_char_p, [_VP]),
+    ("pgn_pod5_file_software", C.c_char_p, [_VP]),
+    ("pgn_pod5_file_pod5_version", C.c_char_p, [_VP]),
+    ("pgn_pod5_file_embedded_count", C.c_int, [_VP]),
+    ("pgn_pod5_file_embedded", C.c_int, [_VP, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                         C.POINTER(C.c_int)]),
+    ("pgn_pod5_signal_info", C.c_int, [_VP, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_int),
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    ("pgn_pod5_signal_read", C.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    ("pgn_pod5_write_file", C.c_int, [C.c_char_p, _VP, C.c_int, C.c_uint64, _VP, _VP, _VP, _VP, C.c_uint32,
+                                      C.c_char_p, _VP]),
+    ("pgn_pod5_transcode_file", C.c_int, [_VP, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_uint32, _VP]),
 ]
 
 

@@ -1016,6 +1016,7 @@ const char* pgn_status_string(int s)
     case PGN_ERR_INVALID_ARG: return "Invalid argument";
     case PGN_ERR_HIP: return "HIP runtime error";
     case PGN_ERR_NO_DEVICE: return "No HIP device";
+    case PGN_ERR_IO: return "File I/O failure";
     default: return "Unknown status";
     }
 }

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/pgnano_pod5.h"
+#include "../../include/pgnano_pod5file.h"
 
 namespace {
 
@@ -161,6 +162,8 @@ static int batch_decompress(pgn_pod5_batch* b, size_t n, const uint8_t* d_in, co
 }
 
 extern "C" {
+
+const char* pgn_pod5_last_error(void) { return g_pod5_err; }
 
 int pgn_pod5_batch_create(pgn_ctx* ctx, int codec, uint32_t chunk_size, pgn_pod5_batch** out)
 {
@@ -344,6 +347,163 @@ int pgn_pod5_decompress_rows(pgn_pod5_batch* b, uint32_t row_count, const uint64
         if (first == PGN_OK && hStatus[i] != PGN_OK) first = hStatus[i];
     }
     return first;
+}
+
+// pgnano_pod5file.h: `copy --pgnano | --VBZ` of a file's signal table.  Device-resident between the
+// two launches: blobs up -> batched decode into one sample buffer -> batched encode -> device-side
+// pack -> packed blobs down.
+int pgn_pod5_transcode_file(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
+                            int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats)
+{
+    if (!ctx || !in_path || !out_path || dst_signal_type < PGN_POD5_SIGNAL_UNCOMPRESSED ||
+        dst_signal_type > PGN_POD5_SIGNAL_PGNANO || pgnano_variant < PGN_VARIANT_C5 || pgnano_variant > PGN_VARIANT_VBZ0)
+        return PGN_ERR_INVALID_ARG;
+    pgn_pod5_file* f = nullptr;
+    int rc = pgn_pod5_file_open(in_path, &f);
+    if (rc) {
+        snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", pgn_pod5_file_error());
+        return rc;
+    }
+    uint64_t rows = 0, dataBytes = 0, total = 0;
+    uint32_t nb = 0;
+    int srcType = 0;
+    pgn_pod5_signal_info(f, &rows, &nb, &srcType, &dataBytes, &total);
+    std::vector<uint8_t> ids(16 * rows), data(dataBytes), outData;
+    std::vector<uint32_t> samples(rows);
+    std::vector<uint64_t> offs(rows + 1), outOffs(rows + 1, 0);
+    pgn_pod5_signal_read(f, ids.data(), samples.data(), offs.data(), data.data());
+    const int srcCodec = srcType == PGN_POD5_SIGNAL_VBZ ? PGN_POD5_CODEC_VBZ : pgnano_variant;
+    const int dstCodec = dst_signal_type == PGN_POD5_SIGNAL_VBZ ? PGN_POD5_CODEC_VBZ : pgnano_variant;
+    const size_t n = (size_t)rows;
+    float decMs = 0, encMs = 0;
+    uint8_t* d = nullptr;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    const hipStream_t stream = (hipStream_t)pgn_ctx_stream(ctx);
+    pgn_pod5_batch src, dst;
+    src.ctx = dst.ctx = ctx;
+    src.stream = dst.stream = stream;
+    src.codec = srcCodec;
+    dst.codec = dstCodec;
+    auto body = [&]() -> int {
+        if (n >= (1u << 31)) return PGN_ERR_UNSUPPORTED;
+        for (size_t i = 0; i < n; i++)
+            if (samples[i] > PGN_MAX_CHUNK_SAMPLES) {
+                snprintf(g_pod5_err, sizeof(g_pod5_err), "row %zu: %u samples above PGN_MAX_CHUNK_SAMPLES", i,
+                         samples[i]);
+                return PGN_ERR_UNSUPPORTED;
+            }
+        if (n == 0) return PGN_OK;
+        uint64_t capTotal = 0;
+        for (size_t i = 0; i < n; i++) capTotal += chunk_cap(dstCodec, samples[i]);
+        // device: samples | sample offsets | counts | status | blobs in | in offsets | in sizes |
+        //         blobs out (capacity-spaced) | out offsets | caps | sizes | packed offsets | first | packed
+        const size_t oSamples = 0, oSoff = up256(2 * total), oCnt = oSoff + up256(8 * n), oStatus = oCnt + up256(4 * n),
+                     oIn = oStatus + up256(4 * n), oIoff = oIn + up256(dataBytes), oIsz = oIoff + up256(8 * n),
+                     oOut = oIsz + up256(8 * n), oOoff = oOut + up256(capTotal), oCaps = oOoff + up256(8 * n),
+                     oSizes = oCaps + up256(8 * n), oPoff = oSizes + up256(8 * n), oFirst = oPoff + up256(8 * (n + 1)),
+                     oPacked = oFirst + 256, devBytes = oPacked + up256(capTotal);
+        P5CHK(hipMalloc((void**)&d, devBytes));
+        for (auto& e : ev) P5CHK(hipEventCreate(&e));
+        // per-row arrays, staged in one host block
+        std::vector<uint64_t> meta(6 * n + 1);
+        uint64_t *hSoff = meta.data(), *hIoff = hSoff + n, *hIsz = hIoff + n, *hOoff = hIsz + n, *hCaps = hOoff + n;
+        uint32_t* hCnt = (uint32_t*)(hCaps + n);
+        uint64_t so = 0, oo = 0;
+        for (size_t i = 0; i < n; i++) {
+            hSoff[i] = so;
+            so += samples[i];
+            hIoff[i] = offs[i];
+            hIsz[i] = offs[i + 1] - offs[i];
+            hCaps[i] = chunk_cap(dstCodec, samples[i]);
+            hOoff[i] = oo;
+            oo += hCaps[i];
+            hCnt[i] = samples[i];
+        }
+        P5CHK(hipMemcpyAsync(d + oSoff, hSoff, 8 * n, hipMemcpyHostToDevice, stream));
+        P5CHK(hipMemcpyAsync(d + oCnt, hCnt, 4 * n, hipMemcpyHostToDevice, stream));
+        P5CHK(hipMemcpyAsync(d + oOoff, hOoff, 8 * n, hipMemcpyHostToDevice, stream));
+        P5CHK(hipMemcpyAsync(d + oCaps, hCaps, 8 * n, hipMemcpyHostToDevice, stream));
+        if (srcType == PGN_POD5_SIGNAL_UNCOMPRESSED) {
+            for (size_t i = 0; i < n; i++)
+                if (hIsz[i] != 2ull * samples[i]) return PGN_ERR_CORRUPT;
+            if (dataBytes) P5CHK(hipMemcpyAsync(d + oSamples, data.data(), dataBytes, hipMemcpyHostToDevice, stream));
+        } else {
+            if (dataBytes) P5CHK(hipMemcpyAsync(d + oIn, data.data(), dataBytes, hipMemcpyHostToDevice, stream));
+            P5CHK(hipMemcpyAsync(d + oIoff, hIoff, 8 * n, hipMemcpyHostToDevice, stream));
+            P5CHK(hipMemcpyAsync(d + oIsz, hIsz, 8 * n, hipMemcpyHostToDevice, stream));
+            P5CHK(hipEventRecord(ev[0], stream));
+            int r = batch_decompress(&src, n, d + oIn, (const uint64_t*)(d + oIoff), (const uint64_t*)(d + oIsz),
+                                     (int16_t*)(d + oSamples), (const uint64_t*)(d + oSoff),
+                                     (const uint32_t*)(d + oCnt), (int32_t*)(d + oStatus));
+            if (r) return r;
+            P5CHK(hipEventRecord(ev[1], stream));
+            std::vector<int32_t> st(n);
+            P5CHK(hipMemcpyAsync(st.data(), d + oStatus, 4 * n, hipMemcpyDeviceToHost, stream));
+            P5CHK(hipStreamSynchronize(stream));
+            P5CHK(hipEventElapsedTime(&decMs, ev[0], ev[1]));
+            for (size_t i = 0; i < n; i++)
+                if (st[i] != PGN_OK) {
+                    snprintf(g_pod5_err, sizeof(g_pod5_err), "row %zu: decode status %d", i, st[i]);
+                    return st[i];
+                }
+        }
+        if (dst_signal_type == PGN_POD5_SIGNAL_UNCOMPRESSED) {
+            outData.resize(2 * total);
+            if (total) P5CHK(hipMemcpyAsync(outData.data(), d + oSamples, 2 * total, hipMemcpyDeviceToHost, stream));
+            P5CHK(hipStreamSynchronize(stream));
+            for (size_t i = 0; i < n; i++) outOffs[i + 1] = outOffs[i] + 2ull * samples[i];
+            return PGN_OK;
+        }
+        P5CHK(hipEventRecord(ev[2], stream));
+        int r = batch_compress(&dst, n, (const int16_t*)(d + oSamples), (const uint64_t*)(d + oSoff),
+                               (const uint32_t*)(d + oCnt), d + oOut, (const uint64_t*)(d + oOoff),
+                               (const uint64_t*)(d + oCaps), (uint64_t*)(d + oSizes), (int32_t*)(d + oStatus));
+        if (r) return r;
+        P5CHK(hipEventRecord(ev[3], stream));
+        hipLaunchKernelGGL(pod5_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)(d + oSizes),
+                           (const int32_t*)(d + oStatus), (uint64_t*)(d + oPoff), (uint32_t*)(d + oFirst), (uint32_t)n);
+        hipLaunchKernelGGL(pod5_pack_kernel, dim3((unsigned)n), dim3(64), 0, stream, (const uint8_t*)(d + oOut),
+                           (const uint64_t*)(d + oOoff), (const uint64_t*)(d + oPoff), d + oPacked, (uint32_t)n);
+        P5CHK(hipGetLastError());
+        uint32_t first = 0;
+        P5CHK(hipMemcpyAsync(outOffs.data(), d + oPoff, 8 * (n + 1), hipMemcpyDeviceToHost, stream));
+        P5CHK(hipMemcpyAsync(&first, d + oFirst, 4, hipMemcpyDeviceToHost, stream));
+        P5CHK(hipStreamSynchronize(stream));
+        P5CHK(hipEventElapsedTime(&encMs, ev[2], ev[3]));
+        if (first < n) {
+            int32_t s = 0;
+            P5CHK(hipMemcpy(&s, d + oStatus + 4 * (size_t)first, 4, hipMemcpyDeviceToHost));
+            snprintf(g_pod5_err, sizeof(g_pod5_err), "row %u: encode status %d", first, s);
+            return s ? s : PGN_ERR_INVALID_ARG;
+        }
+        outData.resize(outOffs[n]);
+        if (outOffs[n]) P5CHK(hipMemcpyAsync(outData.data(), d + oPacked, outOffs[n], hipMemcpyDeviceToHost, stream));
+        P5CHK(hipStreamSynchronize(stream));
+        return PGN_OK;
+    };
+    rc = body();
+    if (d) {
+        (void)hipStreamSynchronize(stream);
+        (void)hipFree(d);
+    }
+    for (auto& e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (rc == PGN_OK)
+    {
+        rc = pgn_pod5_write_file(out_path, f, dst_signal_type, rows, ids.data(), samples.data(), outOffs.data(),
+                                 outData.data(), rows_per_batch, nullptr, nullptr);
+        if (rc) snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", pgn_pod5_file_error());
+    }
+    if (rc == PGN_OK && stats) {
+        stats->rows = rows;
+        stats->samples = total;
+        stats->in_bytes = dataBytes;
+        stats->out_bytes = outOffs[n];
+        stats->decode_ms = decMs;
+        stats->encode_ms = encMs;
+    }
+    pgn_pod5_file_close(f);
+    return rc;
 }
 
 }  // extern "C"

@@ -12,9 +12,10 @@ Tables are pyarrow tables with the POD5 signal-table columns (signal_table_schem
 ``read_id`` (16-byte uuid), ``signal`` (large_binary: the compressed chunk) and ``samples``
 (uint32).  The signal field carries the codec as its extension name, ``minknow.vbz`` or
 ``pgnano.signal`` (types.cpp), in the field metadata.  :func:`read_pod5_signal_table` extracts the
-signal table embedded in a combined POD5 file (pod5/docs/SPECIFICATION.md "Combined file layout");
-writing a combined POD5 file (footer flatbuffer) is not implemented -- :func:`write_signal_table`
-writes the table as an Arrow IPC file.
+signal table embedded in a combined POD5 file as a pyarrow table, for callers that work in Arrow.
+The file-to-file path needs no Arrow: :mod:`.pod5_file` (include/pgnano_pod5file.h) parses and writes
+the combined layout, the footer flatbuffer and the signal table's Arrow IPC file natively, and
+``main`` uses it when both paths are ``.pod5`` files.
 """
 from __future__ import annotations
 
@@ -194,7 +195,8 @@ def read_signal_table(path: str):
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description="Transcode the signal table of a POD5 (or Arrow) file on the GPU")
     ap.add_argument("input", help="combined .pod5 file, or an Arrow IPC signal table")
-    ap.add_argument("output", nargs="?", help="Arrow IPC file for the transcoded signal table")
+    ap.add_argument("output", nargs="?", help="combined .pod5 file (native writer, other tables copied), or an "
+                                              "Arrow IPC file for the transcoded signal table")
     g = ap.add_mutually_exclusive_group()
     g.add_argument("--pgnano", action="store_true", help="write pgnano blobs (default)")
     g.add_argument("--VBZ", action="store_true", help="write VBZ blobs")
@@ -202,6 +204,11 @@ def main(argv=None) -> int:
     ap.add_argument("--check", action="store_true", help="run the double conversion on a VBZ input")
     ap.add_argument("--device", type=int, default=0)
     a = ap.parse_args(argv)
+    if a.input.endswith(".pod5") and a.output and a.output.endswith(".pod5") and not a.check:
+        from .pod5_file import transcode_pod5
+
+        print(json.dumps(transcode_pod5(a.input, a.output, "vbz" if a.VBZ else "pgnano", a.variant, a.device)))
+        return 0
     t = read_pod5_signal_table(a.input) if a.input.endswith(".pod5") else read_signal_table(a.input)
     if a.check:
         print(json.dumps(double_conversion(t, a.device, a.variant)))

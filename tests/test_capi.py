@@ -1,4 +1,4 @@
-"""The C ABI library loads and exports every symbol include/pgnano_hip.h declares (no GPU needed)."""
+"""The C ABI library loads and exports every symbol include/*.h declares (no GPU needed)."""
 import ctypes as C
 import os
 import re
@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     names = set()
-    for h in ("pgnano_hip.h", "pgnano_pod5.h"):
+    for h in ("pgnano_hip.h", "pgnano_pod5.h", "pgnano_pod5file.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(pgn_[a-z0-9_]+)\s*\(", src))

@@ -1,0 +1,136 @@
+"""GPU: POD5 file transcoding (`copy --pgnano` / `copy --VBZ` on a combined file) through the C ABI
+(include/pgnano_pod5file.h), on the reference's own fixture (tests/golden/multi_fast5_zip_v3.pod5).
+
+Parity: the pgnano blobs written to the file are the golden C5 blobs of the fixture's chunks (whose
+streams are pinned by the compiled reference, tests/test_oracle_ref.py), the VBZ column that comes
+back from the double conversion is the reference writer's bytes, and the decoded samples are the
+golden signal digests."""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from _golden import HERE as GOLDEN, c5_blobs, golden
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIXTURE = os.path.join(GOLDEN, "multi_fast5_zip_v3.pod5")
+
+
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def codec():
+    from rawnanoporesignalcompression_amd import PGNanoCodec
+
+    c = PGNanoCodec(0)
+    yield c
+    c.close()
+
+
+def _other_tables(path):
+    from rawnanoporesignalcompression_amd.pod5_file import Pod5File
+
+    raw = open(path, "rb").read()
+    with Pod5File(path) as f:
+        return {k: raw[o:o + ln] for k, o, ln in f.embedded if k != "signal"}, f.file_identifier
+
+
+@pytest.mark.parametrize("rows_per_batch", [100, 4])
+def test_transcode_fixture_to_pgnano_is_golden(codec, tmp_path, rows_per_batch):
+    from rawnanoporesignalcompression_amd.pod5_file import Pod5File, transcode_pod5
+
+    out = str(tmp_path / "pg.pod5")
+    st = transcode_pod5(FIXTURE, out, "pgnano", codec=codec, rows_per_batch=rows_per_batch)
+    g = golden()
+    assert st["rows"] == 22 and st["samples"] == g["real_totals"]["samples"]
+    assert abs(st["bits_per_sample"] - g["real_totals"]["c5_bits_per_sample"]) < 1e-9
+    with Pod5File(out) as f:
+        assert f.signal_type == "pgnano" and f.batches == -(-22 // rows_per_batch)
+        t = f.signal_table()
+    assert [sha(t.blob(i)) for i in range(22)] == [c["c5_sha256"] for c in g["real"]]
+    keep = c5_blobs()
+    assert t.blob(0) == keep["real0"] and t.blob(1) == keep["real1"]
+    assert [r.tobytes().hex() for r in t.read_ids] == [c["read_id"] for c in g["real"]]
+    assert _other_tables(out) == _other_tables(FIXTURE)
+
+
+def test_double_conversion_file_level(codec, tmp_path):
+    """double_conversion.py:37-69 on files: VBZ -> pgnano -> VBZ gives the reference writer's bytes."""
+    from rawnanoporesignalcompression_amd.pod5_file import Pod5File, transcode_pod5
+
+    mid, back = str(tmp_path / "mid.pod5"), str(tmp_path / "back.pod5")
+    transcode_pod5(FIXTURE, mid, "pgnano", codec=codec)
+    st = transcode_pod5(mid, back, "vbz", codec=codec)
+    with Pod5File(FIXTURE) as a, Pod5File(back) as b:
+        ta, tb = a.signal_table(), b.signal_table()
+        assert b.signal_type == "vbz" and st["out_bytes"] == a.data_bytes
+    for k in ("read_ids", "samples", "offsets", "data"):
+        assert np.array_equal(getattr(ta, k), getattr(tb, k)), k
+    assert _other_tables(back) == _other_tables(FIXTURE)
+
+
+def test_uncompressed_legs(codec, tmp_path):
+    """VBZ -> uncompressed gives the golden samples; uncompressed -> pgnano gives the golden blobs."""
+    from rawnanoporesignalcompression_amd.pod5_file import Pod5File, transcode_pod5
+
+    unc, pg = str(tmp_path / "unc.pod5"), str(tmp_path / "pg.pod5")
+    st = transcode_pod5(FIXTURE, unc, "uncompressed", codec=codec)
+    assert st["encode_ms"] == 0 and st["out_bytes"] == 2 * st["samples"]
+    g = golden()
+    with Pod5File(unc) as f:
+        assert f.signal_type == "uncompressed"
+        t = f.signal_table()
+    assert [sha(t.blob(i)) for i in range(22)] == [c["signal_sha256"] for c in g["real"]]
+    st = transcode_pod5(unc, pg, "pgnano", codec=codec)
+    assert st["decode_ms"] == 0
+    with Pod5File(pg) as f:
+        t = f.signal_table()
+    assert [sha(t.blob(i)) for i in range(22)] == [c["c5_sha256"] for c in g["real"]]
+
+
+@pytest.mark.parametrize("variant", ["C4", "C1", "VBZ0"])
+def test_transcode_variants_match_oracle(codec, tmp_path, variant):
+    import _oracle as O
+    from rawnanoporesignalcompression_amd.pod5_file import Pod5File, transcode_pod5
+
+    pg, back = str(tmp_path / "pg.pod5"), str(tmp_path / "back.pod5")
+    transcode_pod5(FIXTURE, pg, "pgnano", variant=variant, codec=codec)
+    with Pod5File(FIXTURE) as a, Pod5File(pg) as b:
+        src, t = a.signal_table(), b.signal_table()
+    for i in (0, 7, 21):
+        rc, x = O.vbz_decompress(src.blob(i), int(src.samples[i]))
+        assert rc == 0
+        rc, blob = O.variant_compress(variant, x)[:2]
+        assert rc == 0 and t.blob(i) == blob, (variant, i)
+    transcode_pod5(pg, back, "vbz", variant=variant, codec=codec)
+    with Pod5File(back) as b:
+        assert np.array_equal(b.signal_table().data, src.data)
+
+
+def test_transcode_errors(codec, tmp_path):
+    from rawnanoporesignalcompression_amd import PGNanoError
+    from rawnanoporesignalcompression_amd.pod5_file import transcode_pod5
+
+    with pytest.raises(PGNanoError) as e:
+        transcode_pod5(str(tmp_path / "missing.pod5"), str(tmp_path / "x.pod5"), codec=codec)
+    assert e.value.status == 13
+    # pgnano blobs decoded as VBZ0 blobs are refused with a decode status, nothing is written
+    pg = str(tmp_path / "pg.pod5")
+    transcode_pod5(FIXTURE, pg, "pgnano", codec=codec)
+    with pytest.raises(PGNanoError):
+        transcode_pod5(pg, str(tmp_path / "bad.pod5"), "vbz", variant="C2", codec=codec)
+    assert not os.path.exists(str(tmp_path / "bad.pod5"))
+
+
+def test_c_program_double_conversion(tmp_path):
+    exe = os.path.join(ROOT, "rawnanoporesignalcompression_amd", "_build", "test_pod5_file")
+    assert os.path.exists(exe), "build it with make -C rawnanoporesignalcompression_amd"
+    r = subprocess.run([exe, FIXTURE, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    print(r.stdout)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert "identical" in r.stdout
