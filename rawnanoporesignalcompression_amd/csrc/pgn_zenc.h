@@ -163,6 +163,32 @@ __device__ inline uint32_t wave_back_count(const uint8_t* src, uint32_t a, uint3
     return lim;
 }
 
+// The no-match visit recurrence of ZSTD_compressBlock_fast (ip += ((ip - anchor) >> 7) + 2), as
+// e = ip - anchor + 256 -> e + (e >> 7), only ever starts at e = 256 (a round after a match or a
+// repcode run: ip == anchor) or 257 (the first block of a frame: ip = 1, anchor = 0).  Both chains
+// are tabulated once (constant memory, read through the caches), so a round's 64 visit positions are
+// one coalesced load instead of 64 dependent scalar steps.
+constexpr int kChainLen = 1344;
+struct VisitChains {
+    uint32_t e[2][kChainLen];
+};
+constexpr VisitChains make_visit_chains()
+{
+    VisitChains c{};
+    for (int s = 0; s < 2; s++) {
+        uint32_t e = 256u + (uint32_t)s;
+        for (int i = 0; i < kChainLen; i++) {
+            c.e[s][i] = e;
+            e += e >> 7;
+        }
+    }
+    return c;
+}
+constexpr VisitChains kVisitChainsHost = make_visit_chains();
+// a round reads entries ci .. ci + 64; the chains must outrun any block (e <= 2^20 + 256)
+static_assert(kVisitChainsHost.e[0][kChainLen - 65] > (1u << 20) + 512u, "visit chain too short");
+__constant__ VisitChains kVisitChains = make_visit_chains();
+
 // Match search (ZSTD_compressBlock_fast, libzstd 1.4.x) speculated over 64 consecutive visits.
 // The visit positions follow a data-independent recurrence until a match is found, so lane k takes
 // visit k of the round: it hashes its two positions, reads the table (entries (tag << 17) | idx,
@@ -203,18 +229,13 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
     lds_sync();
-    // positions of the 64 visits starting at p (the no-match recurrence q += ((q - anchor) >> 7) + 2;
-    // scalar, with v_writelane).  With e = q - anchor + 256 it is e += e >> 7: two scalar
-    // instructions per visit.
-    auto positions = [&](int32_t p, int32_t& pkOut, int32_t& pNextOut) {
-        uint32_t e = (uint32_t)(p - anchor) + 256u, ek = 0;
-#pragma unroll
-        for (int k = 0; k < 64; k++) {
-            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(ek) : "s"(e), "i"(k));
-            e += e >> 7;
-        }
-        pkOut = (int32_t)ek + (anchor - 256);
-        pNextOut = (int32_t)e + (anchor - 256);
+    // positions of the 64 visits at chain index ci (the no-match recurrence, tabulated in
+    // kVisitChains; the chain restarts at index 0 after every match)
+    uint32_t chain = (start == 0) ? 1u : 0u, ci = 0;
+    auto positions = [&](uint32_t c, int32_t& pkOut, int32_t& pNextOut) {
+        const uint32_t* E = kVisitChains.e[chain];
+        pkOut = (int32_t)E[c + lane] + (anchor - 256);
+        pNextOut = (int32_t)E[c + 64] + (anchor - 256);
     };
     int32_t pk = 0, pNext = 0;
     uint64_t v8 = 0;    // bytes pk .. pk+7: both hashes and the current-position words
@@ -229,7 +250,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     while (ip0 + 1 < ilimit) {
         rounds++;
         if (!havePk) {
-            positions(ip0, pk, pNext);
+            positions(ci, pk, pNext);
             loads(pk, v8, repw);
         }
         havePk = false;
@@ -253,7 +274,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         // the next round's visits and their bytes, assuming this one finds no match (overlaps the
         // table reads)
         int32_t pkN, pNextN;
-        positions(pNext, pkN, pNextN);
+        positions(ci + 64, pkN, pNextN);
         uint64_t v8N = 0;
         uint32_t repwN = 0;
         loads(pkN, v8N, repwN);
@@ -329,6 +350,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             wave_sync();
             if (vmask == ~0ull) {
                 ip0 = pNext;
+                ci += 64;
                 pk = pkN;
                 pNext = pNextN;
                 v8 = v8N;
@@ -374,6 +396,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         nbSeq++;
         ip0 = ipm + (int32_t)mLength;
         anchor = ip0;
+        chain = 0;
+        ci = 0;
         if (ip0 <= ilimit) {
             if (lane == 0) {
                 const uint64_t wa = ld64u(src + cur0 + 1), wb = ld64u(src + ip0 - 2);
