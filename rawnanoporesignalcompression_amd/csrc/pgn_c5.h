@@ -286,8 +286,8 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
 // Returns 0 ok, 1 out-of-bounds; *consumed = one past the last Lhigh byte.
 // ---------------------------------------------------------------------------------------------
 struct MergeLds {
-    // one step's S, M and class-3 values as 16-bit entries with their class offsets added, back to
-    // back: S (one nibble per entry) from a 16-byte aligned stream byte, then M likewise, then L | H << 8.
+    // one step's S, M and class-3 values as 16-bit deltas (class offsets added, zig-zag decoded), back
+    // to back: S (one nibble per entry) from a 16-byte aligned stream byte, then M likewise, then L | H << 8.
     // A step has at most 1024 of them together, plus the alignment slack of two windows.
     alignas(16) uint16_t V[1024 + 64 + 32 + 32];
     uint16_t zero[2];  // what a class-0 sample reads
@@ -302,7 +302,13 @@ __device__ __forceinline__ uint64_t stage_bytes(uint8_t* W, const uint8_t* in, u
     return a0;
 }
 
-// 16 bytes of nibbles -> 32 entries (low nibble first) + add, written at d
+// two zig-zag codes -> their 16-bit deltas (packed)
+__device__ __forceinline__ uint32_t zz_dec16x2(uint32_t w)
+{
+    const pgn_u16x2 x = as_u16x2(w);
+    return as_u32((x >> (pgn_u16x2){1, 1}) ^ ((pgn_u16x2){0, 0} - (x & (pgn_u16x2){1, 1})));
+}
+// 16 bytes of nibbles -> 32 entries (low nibble first) + add, zig-zag decoded, written at d
 __device__ __forceinline__ void put_nibbles16(uint16_t* d, const uint4& v, uint32_t add2)
 {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -312,7 +318,7 @@ __device__ __forceinline__ void put_nibbles16(uint16_t* d, const uint4& v, uint3
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t y = __builtin_amdgcn_perm(0u, w[j], 0x0C000C00u + 0x00010001u * (uint32_t)k);  // byte k twice
-            o[4 * j + k] = ((y & 0xFu) | ((y >> 4) & 0x000F0000u)) + add2;
+            o[4 * j + k] = zz_dec16x2(((y & 0xFu) | ((y >> 4) & 0x000F0000u)) + add2);
         }
     uint4* q = (uint4*)d;
     q[0] = make_uint4(o[0], o[1], o[2], o[3]);
@@ -320,15 +326,15 @@ __device__ __forceinline__ void put_nibbles16(uint16_t* d, const uint4& v, uint3
     q[2] = make_uint4(o[8], o[9], o[10], o[11]);
     q[3] = make_uint4(o[12], o[13], o[14], o[15]);
 }
-// 16 bytes -> 16 entries + add, written at d
+// 16 bytes -> 16 entries + add, zig-zag decoded, written at d
 __device__ __forceinline__ void put_bytes16(uint16_t* d, const uint4& v, uint32_t add2)
 {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[8];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        o[2 * j] = __builtin_amdgcn_perm(0u, w[j], 0x0C010C00u) + add2;
-        o[2 * j + 1] = __builtin_amdgcn_perm(0u, w[j], 0x0C030C02u) + add2;
+        o[2 * j] = zz_dec16x2(__builtin_amdgcn_perm(0u, w[j], 0x0C010C00u) + add2);
+        o[2 * j + 1] = zz_dec16x2(__builtin_amdgcn_perm(0u, w[j], 0x0C030C02u) + add2);
     }
     uint4* q = (uint4*)d;
     q[0] = make_uint4(o[0], o[1], o[2], o[3]);
@@ -336,31 +342,38 @@ __device__ __forceinline__ void put_bytes16(uint16_t* d, const uint4& v, uint32_
 }
 
 // Merge step over 1024 samples: lane l decodes the 16 consecutive samples t + 16l .. t + 16l + 15,
-// whose 16 keys are its own key word.  Every class has a staged 16-bit window with its offset
-// already added (class 0 reads a zero), and the lane's places in them are the step's fills plus
-// the class counts of the lanes below it (one packed DPP scan); so a sample is one LDS read at its
-// class's running place, a running 16-bit sum, and a second scan carries the sum across lanes.
-// Outputs leave as two 16-byte stores per lane.
+// whose 16 keys are its own key word.  Every class has a staged 16-bit window of deltas (offsets
+// added and zig-zag decoded at staging; class 0 reads a zero), and the lane's first place in each is
+// the step's fill plus the class counts of the lanes below it (one packed DPP scan).  Sample m's
+// place is its class's first place plus twice the number of earlier samples of its class in the key
+// word: one popcount of the class's pair mask below m (both bits of a pair set, so the count comes
+// out doubled = the entry's byte stride), the mask and the first place picked by a two-level bit
+// select on the sample's two key bits.  So a sample is one LDS read and a running 16-bit sum, and a
+// second scan carries the sum across lanes.  Outputs leave as two 16-byte stores per lane.
 __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, uint32_t pS, uint32_t pM, uint32_t pL,
                                            uint32_t& carry, int16_t* __restrict__ out, uint32_t t, uint32_t n, bool full)
 {
     const uint32_t lane = (uint32_t)lane_id();
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&W);
     constexpr uint32_t pZ = (uint32_t)__builtin_offsetof(MergeLds, zero);
+    const uint32_t klo = kw & 0x55555555u, khi = (kw >> 1) & 0x55555555u;
+    const uint32_t dS = (klo & ~khi) * 3u, dM = (khi & ~klo) * 3u, dL = (klo & khi) * 3u;
     uint32_t acc = 0;
     uint32_t w[8];  // running sums, two 16-bit samples per word
 #pragma unroll
     for (int m = 0; m < 16; m++) {
-        // the class bits as all-ones / all-zero masks: a two-level bit-select picks the place
+        // the class bits as all-ones / all-zero masks
         const uint32_t b0 = (uint32_t)(((int32_t)(kw << (31 - 2 * m))) >> 31);
         const uint32_t b1 = (uint32_t)(((int32_t)(kw << (30 - 2 * m))) >> 31);
         const uint32_t lo = (pS & b0) | (pZ & ~b0), hi = (pL & b0) | (pM & ~b0);
-        const uint32_t at = (hi & b1) | (lo & ~b1);
+        uint32_t at = (hi & b1) | (lo & ~b1);
+        if (m > 0) {
+            const uint32_t dlo = dS & b0, dhi = (dL & b0) | (dM & ~b0);
+            const uint32_t d = ((dhi & b1) | (dlo & ~b1)) & ((1u << (2 * m)) - 1u);
+            at += (uint32_t)__builtin_popcount(d);
+        }
         const uint32_t v = *reinterpret_cast<const uint16_t*>(wb + at);
-        pS += b0 & ~b1 & 2u;
-        pM += b1 & ~b0 & 2u;
-        pL += b0 & b1 & 2u;
-        acc += (uint32_t)zz_dec16((uint16_t)v);
+        acc += v;
         if (m & 1) w[m >> 1] |= acc << 16;
         else w[m >> 1] = acc & 0xFFFFu;
         if (m % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // at most 4 places read ahead (VGPRs)
@@ -435,11 +448,11 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
             }
             if (lane < nbS) put_nibbles16(W.V + 32u * lane, vS, add1);
             if (lane < nbM) put_bytes16(W.V + eM + 16u * lane, vM, add2);
-            if (lane < nl) W.V[eL + lane] = (uint16_t)((lb | (hb << 8)) + ClassOffsets<C4>::o3);
+            if (lane < nl) W.V[eL + lane] = zz_dec16((uint16_t)((lb | (hb << 8)) + ClassOffsets<C4>::o3));
             for (uint32_t b = lane + 64; b < nbS; b += 64) put_nibbles16(W.V + 32u * b, gld<uint4>(in + aS0 + 16u * b), add1);
             for (uint32_t b = lane + 64; b < nbM; b += 64) put_bytes16(W.V + eM + 16u * b, gld<uint4>(in + aM0 + 16u * b), add2);
             for (uint32_t i = lane + 64; i < nl; i += 64)
-                W.V[eL + i] = (uint16_t)(((uint32_t)gb(in + pl + lN + i) | ((uint32_t)gb(in + ph + lN + i) << 8)) + ClassOffsets<C4>::o3);
+                W.V[eL + i] = zz_dec16((uint16_t)(((uint32_t)gb(in + pl + lN + i) | ((uint32_t)gb(in + ph + lN + i) << 8)) + ClassOffsets<C4>::o3));
         }
         lds_sync();
         // LDS byte places of my first value of each class

@@ -261,30 +261,31 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             int32_t p = entry;
             StgBits r;
             stg_init(r, lane, p - b8 - tli);
-            uint32_t i = 0;
-            while (ballot(i + 4 <= cnt)) {
+            // Lanes that are done keep decoding at their fixed position (their reader stays valid: a
+            // fixed position refills at most once) and store nothing; the trip counts are wave-uniform,
+            // so the loops have no divergent region and the loop-carried state needs no copies.
+            const uint32_t my4 = cnt >> 2, myTail = cnt & 3u;
+            const uint32_t n4 = wave_max(my4), nTail = wave_max(myTail);
+            for (uint32_t g = 0; g < n4; g++) {
                 P.count(7);
-                if (i + 4 <= cnt) {
-                    uint32_t word = 0;
+                const bool act = g < my4;
+                uint32_t word = 0;
 #pragma unroll
-                    for (int u = 0; u < 2; u++) {
-                        uint32_t e1, e2;
-                        stg_entry2(r, lane, p - b8 - tli, tmask, tli, e1, e2);
-                        p -= (int32_t)(e1 >> 8) + (int32_t)(e2 >> 8);
-                        word |= ((e1 & 0xFFu) | ((e2 & 0xFFu) << 8)) << (16 * u);
-                    }
-                    gst<uint32_t>(out + i, word);
-                    i += 4;
+                for (int u = 0; u < 2; u++) {
+                    uint32_t e1, e2;
+                    stg_entry2(r, lane, p - b8 - tli, tmask, tli, e1, e2);
+                    p -= act ? (int32_t)(e1 >> 8) + (int32_t)(e2 >> 8) : 0;
+                    word |= ((e1 & 0xFFu) | ((e2 & 0xFFu) << 8)) << (16 * u);
                 }
+                if (act) gst<uint32_t>(out + 4u * g, word);
             }
-            while (ballot(i < cnt)) {
+            out += 4u * my4;
+            for (uint32_t g = 0; g < nTail; g++) {
                 P.count(8);
-                if (i < cnt) {
-                    const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
-                    p -= (int32_t)(e >> 8);
-                    gst<uint8_t>(out + i, (uint8_t)e);
-                    i++;
-                }
+                const bool act = g < myTail;
+                const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
+                p -= act ? (int32_t)(e >> 8) : 0;
+                if (act) gst<uint8_t>(out + g, (uint8_t)e);
             }
         }
         P.mark(8);

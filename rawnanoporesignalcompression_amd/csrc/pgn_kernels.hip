@@ -357,7 +357,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     P.flush();
 }
 
-__global__ __launch_bounds__(64) void dec_merge_kernel(DecArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void dec_merge_kernel(DecArgs a)
 {
     const size_t g = blockIdx.x;
     const size_t c = a.base + g;

@@ -9,7 +9,8 @@
 // Serial stages (tree build, weight FSE, sequence FSE) run on lane 0 with the shared zstd1_* code.
 #pragma once
 #ifndef PGN_AB_SKIP
-#define PGN_AB_SKIP 0  // diagnostic builds (tools/ab_skip.sh): 1 no zstd stage, 2 search only, 3 no Huffman, 4 no bit packing
+#define PGN_AB_SKIP 0  // diagnostic builds (tools/ab_skip.sh): 1 no zstd stage, 2 search only, 3 no Huffman, 4 no bit packing;
+                       // PGN_AB_HLOG=h caps the hash log (table-footprint probe)
 #endif
 #include "pgn_c5.h"
 #include "pgn_wave.h"
@@ -213,6 +214,9 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     start = uni(start);
     end = uni(end);
     hlog = uni(hlog);
+#ifdef PGN_AB_HLOG
+    hlog = hlog > PGN_AB_HLOG ? PGN_AB_HLOG : hlog;  // diagnostic: smaller tables (other matches, not parity)
+#endif
     mls = uni(mls);
     ht = uni(ht);
     tag = uni(tag);
