@@ -72,7 +72,7 @@ __host__ __device__ inline EncLayout enc_layout()
     EncLayout l{};
     size_t o = 0;
     auto take = [&](size_t n) { size_t r = o; o = align_up(o + n + 64, 256); return r; };
-    l.ht = take((size_t)8 << 15);
+    l.ht = take((size_t)4 << 15);
     l.lit = take(z1::kMaxSrc);
     l.seqs = take(sizeof(z1::Seq) * kMaxEncSeq);
     l.codes = take(3 * (size_t)kMaxEncSeq);
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
     const EncLayout lay = enc_layout();
     uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
     EncScratch S;
-    S.ht = (uint64_t*)(sbase + lay.ht);
+    S.ht = (uint32_t*)(sbase + lay.ht);
     S.seqs = (z1::Seq*)(sbase + lay.seqs);
     S.codes = sbase + lay.codes;
     S.lit = sbase + lay.lit;
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
         const uint32_t n = a.sizes[g * kStreams + s];
         if (a.sizes[g * kStreams] == ~0u) continue;  // unsupported chunk
         if (++epoch >= kTagEpochs) {  // tag space exhausted: clear the table once
-            for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
+            for (uint32_t i = (uint32_t)lane; i < (1u << 13); i += 64) gst<uint4>(S.ht + 4 * i, make_uint4(0, 0, 0, 0));
             epoch = 1;
             wave_sync();
         }
@@ -628,7 +628,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
     const EncLayout lay = enc_layout();
     uint8_t* sbase = a.slotScratch + (size_t)blockIdx.x * a.slotBytes;
     EncScratch S;
-    S.ht = (uint64_t*)(sbase + lay.ht);
+    S.ht = (uint32_t*)(sbase + lay.ht);
     S.seqs = (z1::Seq*)(sbase + lay.seqs);
     S.codes = sbase + lay.codes;
     S.lit = sbase + lay.lit;
@@ -706,7 +706,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
         for (int s = 0; s < nf; s++) {
             if (s < nf - 1) off += 8;  // length prefixes of all frames but the last (C5.hpp:429-462)
             if (++epoch >= kTagEpochs) {  // tag space exhausted: clear the table once
-                for (uint32_t i = (uint32_t)lane; i < (1u << 15); i += 64) S.ht[i] = 0;
+                for (uint32_t i = (uint32_t)lane; i < (1u << 13); i += 64) gst<uint4>(S.ht + 4 * i, make_uint4(0, 0, 0, 0));
                 epoch = 1;
                 wave_sync();
             }

@@ -92,7 +92,7 @@ __device__ __forceinline__ uint32_t seg_count(const EncLds& L, int k, int s)
 static __shared__ EncLds sEnc;
 
 struct EncScratch {
-    uint64_t* ht;        // 2^15 hash-table entries: tag << kTagShift | index, and the 4 bytes at that position
+    uint32_t* ht;        // 2^15 hash-table entries: tag << kTagShift | fingerprint of the 4 bytes | index
     z1::Seq* seqs;       // <= stream/4 + 2 sequences
     uint8_t* codes;      // 3 * (stream/4 + 2)
     uint8_t* lit;        // gathered literals (stream bytes)
@@ -130,17 +130,25 @@ __device__ inline uint32_t wave_match_count(const uint8_t* src, uint32_t a, uint
     return n;
 }
 
-// Hash-table entries: a per-slot epoch tag above a 20-bit index (positions of frames up to
-// kMaxFrameSrc = 512 KiB); the table is cleared once per kTagEpochs streams.
-constexpr uint32_t kTagShift = 20;
+// Hash-table entries, 32 bits: a per-slot epoch tag in the top 5 bits (any other tag reads as an
+// empty slot; the table is cleared once per kTagEpochs - 1 frames), the index (position + 1) in the
+// low idxBits (17 for frames up to 128 KiB, 20 up to kMaxFrameSrc = 512 KiB), and between them a
+// fingerprint of MEM_read32 at the position (10 or 7 bits).  A candidate whose fingerprint differs
+// is no match without reading the stream; one whose fingerprint agrees is confirmed by one read of
+// its 4 bytes.  Four bytes per entry keep a slot's table at 2^hashLog x 4 B (32 KiB for the
+// hashLog-13 streams), half of an entry that carries the bytes.
+constexpr uint32_t kTagShift = 27;
 constexpr uint32_t kTagEpochs = 1u << (32 - kTagShift);
-static_assert(z1::kMaxFrameSrc + 2 < (1u << kTagShift), "index field");
-__device__ inline uint32_t tagged(uint32_t tag, uint32_t idx) { return (tag << kTagShift) | idx; }
-// a table entry: the tagged index (position + 1) and MEM_read32 of the position, so that a
-// candidate is tested without reading the stream again
-__device__ inline uint64_t ht_entry(uint32_t tag, uint32_t idx, uint32_t bytes)
+static_assert(z1::kMaxFrameSrc + 2 < (1u << 20), "index field");
+__device__ inline uint32_t ht_idx_bits(uint32_t frameN) { return frameN + 2 < (1u << 17) ? 17u : 20u; }
+// the fingerprint field of the entry for these 4 bytes (bits [idxBits, kTagShift))
+__device__ inline uint32_t ht_fp(uint32_t bytes, uint32_t idxBits)
 {
-    return (uint64_t)tagged(tag, idx) | ((uint64_t)bytes << 32);
+    return ((bytes * 0x9E3779B1u) >> (32u - (kTagShift - idxBits))) << idxBits;
+}
+__device__ inline uint32_t ht_entry(uint32_t tag, uint32_t idx, uint32_t bytes, uint32_t idxBits)
+{
+    return (tag << kTagShift) | ht_fp(bytes, idxBits) | idx;
 }
 
 // ZSTD_hashPtr (mls 5 / 6 / 7) over 8 global bytes
@@ -205,8 +213,8 @@ struct SearchOut {
     uint32_t candIters;  // profile builds: wave iterations of the same-slot loops
 };
 __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ src, uint32_t start, uint32_t end, unsigned hlog,
-                                                   unsigned mls, uint64_t* __restrict__ ht, uint32_t tag,
-                                                   z1::Seq* __restrict__ seqs, uint32_t rep0, uint32_t rep1)
+                                                   unsigned mls, uint32_t* __restrict__ ht, uint32_t tag,
+                                                   z1::Seq* __restrict__ seqs, uint32_t rep0, uint32_t rep1, uint32_t idxBits)
 {
     EncLds& L = sEnc;
     const uint32_t lane = (uint32_t)lane_id();
@@ -223,6 +231,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     seqs = uni(seqs);
     rep0 = uni(rep0);
     rep1 = uni(rep1);
+    idxBits = uni(idxBits);
+    const uint32_t idxMask = (1u << idxBits) - 1u, fpMask = ((1u << kTagShift) - 1u) & ~idxMask;
     const int32_t iend = (int32_t)end, ilimit = (int32_t)end - 8;
     int32_t ip0 = (int32_t)start + (start == 0 ? 1 : 0), anchor = (int32_t)start;
     // ZSTD_compressBlock_fast_generic: repeat offsets beyond the first position are invalidated
@@ -260,13 +270,13 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         havePk = false;
         const bool valid = (pk + 1 < ilimit);
         uint32_t h0 = 0xFFFFFFFFu, h1 = 0xFFFFFFFEu;
-        uint64_t t0 = 0, t1 = 0;
+        uint32_t t0 = 0, t1 = 0;
         uint64_t M0 = 0, M1 = 0;
         if (valid) {
             h0 = z1::hash_word(v8, hlog, mls);
             h1 = z1::hash_word(v8 >> 8, hlog, mls);
-            t0 = gld<uint64_t>(ht + h0);
-            t1 = gld<uint64_t>(ht + h1);
+            t0 = gld<uint32_t>(ht + h0);
+            t1 = gld<uint32_t>(ht + h1);
             atomicOr((unsigned long long*)&L.filt[h0 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
             atomicOr((unsigned long long*)&L.filt[h1 & (kFiltSlots - 1)], (unsigned long long)(1ull << lane));
         }
@@ -292,10 +302,14 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             L.filt[h0 & (kFiltSlots - 1)] = 0;
             L.filt[h1 & (kFiltSlots - 1)] = 0;
         }
-        // value each slot holds at my visit: the latest earlier writer in this round, else the table
-        uint32_t m0 = (((uint32_t)t0 >> kTagShift) == tag) ? ((uint32_t)t0 & ((1u << kTagShift) - 1u)) : 0u;
-        uint32_t m1 = (((uint32_t)t1 >> kTagShift) == tag) ? ((uint32_t)t1 & ((1u << kTagShift) - 1u)) : 0u;
-        uint32_t d0 = (uint32_t)(t0 >> 32), d1 = (uint32_t)(t1 >> 32);
+        // value each slot holds at my visit: the latest earlier writer in this round (its bytes known
+        // exactly), else the table (its fingerprint)
+        const uint32_t fp0 = ht_fp((uint32_t)v8, idxBits), fp1 = ht_fp((uint32_t)(v8 >> 8), idxBits);
+        uint32_t m0 = ((t0 >> kTagShift) == tag) ? (t0 & idxMask) : 0u;
+        uint32_t m1 = ((t1 >> kTagShift) == tag) ? (t1 & idxMask) : 0u;
+        bool fpok0 = ((t0 ^ fp0) & fpMask) == 0, fpok1 = ((t1 ^ fp1) & fpMask) == 0;
+        bool fw0 = false, fw1 = false;
+        uint32_t d0 = 0, d1 = 0;
 #ifdef PGN_PROFILE
         uint32_t myIt = 0;
 #endif
@@ -305,8 +319,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
 #endif
             const int jj = 63 - __builtin_clzll(cand);
             const uint32_t pj = L.vpk[jj];
-            if (L.vh1[jj] == h0) { m0 = pj + 2; d0 = L.vd1[jj]; break; }
-            if (L.vh0[jj] == h0) { m0 = pj + 1; d0 = L.vd0[jj]; break; }
+            if (L.vh1[jj] == h0) { m0 = pj + 2; d0 = L.vd1[jj]; fw0 = true; break; }
+            if (L.vh0[jj] == h0) { m0 = pj + 1; d0 = L.vd0[jj]; fw0 = true; break; }
             cand &= ~(1ull << jj);
         }
         for (uint64_t cand = M1 & below; cand;) {
@@ -315,15 +329,22 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
 #endif
             const int jj = 63 - __builtin_clzll(cand);
             const uint32_t pj = L.vpk[jj];
-            if (L.vh1[jj] == h1) { m1 = pj + 2; d1 = L.vd1[jj]; break; }
-            if (L.vh0[jj] == h1) { m1 = pj + 1; d1 = L.vd0[jj]; break; }
+            if (L.vh1[jj] == h1) { m1 = pj + 2; d1 = L.vd1[jj]; fw1 = true; break; }
+            if (L.vh0[jj] == h1) { m1 = pj + 1; d1 = L.vd0[jj]; fw1 = true; break; }
             cand &= ~(1ull << jj);
         }
         bool rep = false, c0 = false, c1 = false;
+        bool vf0 = false, vf1 = false;  // table candidates whose fingerprint agrees: read their bytes
         if (valid) {
             rep = (off1 > 0) && (repw == (uint32_t)(v8 >> 16));
-            c0 = (m0 > 1) && (d0 == (uint32_t)v8);
-            c1 = (m1 > 1) && (d1 == (uint32_t)(v8 >> 8));
+            c0 = (m0 > 1) && (fw0 ? d0 == (uint32_t)v8 : fpok0);
+            c1 = (m1 > 1) && (fw1 ? d1 == (uint32_t)(v8 >> 8) : fpok1);
+            vf0 = c0 && !fw0;
+            vf1 = c1 && !fw1;
+        }
+        if (ballot(vf0 || vf1)) {
+            if (vf0) c0 = ld32u(src + (m0 - 1)) == (uint32_t)v8;
+            if (vf1) c1 = ld32u(src + (m1 - 1)) == (uint32_t)(v8 >> 8);
         }
 #ifdef PGN_PROFILE
         candIters += wave_max(myIt);
@@ -346,8 +367,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
                 if (L.vh0[jj] == h1 || L.vh1[jj] == h1) w1 = false;
                 cand &= cand - 1;
             }
-            if (w0) gst<uint64_t>(ht + h0, ht_entry(tag, (uint32_t)pk + 1, (uint32_t)v8));
-            if (w1) gst<uint64_t>(ht + h1, ht_entry(tag, (uint32_t)pk + 2, (uint32_t)(v8 >> 8)));
+            if (w0) gst<uint32_t>(ht + h0, (tag << kTagShift) | fp0 | ((uint32_t)pk + 1));
+            if (w1) gst<uint32_t>(ht + h1, (tag << kTagShift) | fp1 | ((uint32_t)pk + 2));
         }
         lds_sync();
         if (!hits) {
@@ -405,8 +426,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         if (ip0 <= ilimit) {
             if (lane == 0) {
                 const uint64_t wa = ld64u(src + cur0 + 1), wb = ld64u(src + ip0 - 2);
-                gst<uint64_t>(ht + z1::hash_word(wa, hlog, mls), ht_entry(tag, cur0 + 2, (uint32_t)wa));
-                gst<uint64_t>(ht + z1::hash_word(wb, hlog, mls), ht_entry(tag, (uint32_t)(ip0 - 2) + 1, (uint32_t)wb));
+                gst<uint32_t>(ht + z1::hash_word(wa, hlog, mls), ht_entry(tag, cur0 + 2, (uint32_t)wa, idxBits));
+                gst<uint32_t>(ht + z1::hash_word(wb, hlog, mls), ht_entry(tag, (uint32_t)(ip0 - 2) + 1, (uint32_t)wb, idxBits));
             }
             if (off2 > 0) {
                 while ((ip0 <= ilimit) && (ld32u(src + ip0) == ld32u(src + ip0 - (int32_t)off2))) {
@@ -416,7 +437,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
                     off1 = t;
                     if (lane == 0) {
                         const uint64_t wr = ld64u(src + ip0);
-                        gst<uint64_t>(ht + z1::hash_word(wr, hlog, mls), ht_entry(tag, (uint32_t)ip0 + 1, (uint32_t)wr));
+                        gst<uint32_t>(ht + z1::hash_word(wr, hlog, mls), ht_entry(tag, (uint32_t)ip0 + 1, (uint32_t)wr, idxBits));
                         seqs[nbSeq].litLength = 0;
                         seqs[nbSeq].offset = 1;
                         seqs[nbSeq].mlBase = rLength - 3;
@@ -1608,7 +1629,8 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
 #else
         if (bs >= 7) {
 #endif
-            const SearchOut so = fast_search_wave(src, start, start + bs, p.hashLog, p.mls, S.ht, tag, S.seqs, rep0, rep1);
+            const SearchOut so = fast_search_wave(src, start, start + bs, p.hashLog, p.mls, S.ht, tag, S.seqs, rep0, rep1,
+                                                      ht_idx_bits(n));
             const uint32_t nbSeq = uni(so.nbSeq), lastLL = uni(so.lastLL);
             P.mark(1);
             P.count(0, uni(so.rounds));
