@@ -334,22 +334,41 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             cand &= ~(1ull << jj);
         }
         bool rep = false, c0 = false, c1 = false;
-        bool vf0 = false, vf1 = false;  // table candidates whose fingerprint agrees: read their bytes
         if (valid) {
             rep = (off1 > 0) && (repw == (uint32_t)(v8 >> 16));
             c0 = (m0 > 1) && (fw0 ? d0 == (uint32_t)v8 : fpok0);
             c1 = (m1 > 1) && (fw1 ? d1 == (uint32_t)(v8 >> 8) : fpok1);
-            vf0 = c0 && !fw0;
-            vf1 = c1 && !fw1;
-        }
-        if (ballot(vf0 || vf1)) {
-            if (vf0) c0 = ld32u(src + (m0 - 1)) == (uint32_t)v8;
-            if (vf1) c1 = ld32u(src + (m1 - 1)) == (uint32_t)(v8 >> 8);
         }
 #ifdef PGN_PROFILE
         candIters += wave_max(myIt);
 #endif
-        const uint64_t hits = ballot(rep || c0 || c1);
+        // The first hit decides the round.  A table candidate there has only its fingerprint checked,
+        // so its bytes are compared by counting the match forward from its first byte -- the count
+        // the match needs anyway, so a true match costs no extra read; a false candidate is dropped
+        // and the next hit taken.
+        uint64_t hits = ballot(rep || c0 || c1);
+        uint32_t fwdKnown = 0;  // forward length of the chosen table candidate from its first byte
+        {
+            const uint64_t fwb0 = ballot(fw0), fwb1 = ballot(fw1);
+            while (hits) {
+                const int ff = __builtin_ctzll(hits);
+                if ((ballot(rep) >> ff) & 1) break;
+                const bool isC0 = (ballot(c0) >> ff) & 1;
+                if (((isC0 ? fwb0 : fwb1) >> ff) & 1) break;  // an earlier visit's write: bytes compared exactly
+                const uint32_t mf = readlane_u32(isC0 ? m0 : m1, ff);
+                const uint32_t ipc = readlane_u32((uint32_t)pk, ff) + (isC0 ? 0u : 1u);
+                const uint32_t nm = wave_match_count(src, ipc, mf - 1, (uint32_t)iend);
+                if (nm >= 4) {
+                    fwdKnown = nm;
+                    break;
+                }
+                if ((int)lane == ff) {
+                    if (isC0) c0 = false;
+                    else c1 = false;
+                }
+                hits = ballot(rep || c0 || c1);
+            }
+        }
         const uint64_t vmask = ballot(valid);
         const int f = hits ? __builtin_ctzll(hits) : 64;
         const int lastCommit = hits ? f : (63 - __builtin_clzll(vmask));
@@ -412,7 +431,9 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             match0 -= (int32_t)back;
             mLength += back;
         }
-        mLength += wave_match_count(src, (uint32_t)ipm + mLength, (uint32_t)match0 + mLength, (uint32_t)iend);
+        // (the forward part starts 4 bytes past the candidate, whatever the backward extension)
+        mLength += fwdKnown ? fwdKnown - 4u
+                            : wave_match_count(src, (uint32_t)ipm + mLength, (uint32_t)match0 + mLength, (uint32_t)iend);
         if (lane == 0) {
             seqs[nbSeq].litLength = (uint32_t)(ipm - anchor);
             seqs[nbSeq].offset = offcode + 1;
