@@ -177,7 +177,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
     S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
     S.maxSeq = kMaxEncSeq;
     S.huf = (uint32_t*)(sbase + lay.huf);
-    uint32_t epoch = a.epochs[blockIdx.x];
+    uint32_t epoch = a.epochs[blockIdx.x];  // table state: epoch tag | written extent << 8 (ht_next_epoch)
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = (size_t)a.nu * G;
@@ -191,15 +191,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
         if (a.base + g >= a.nchunks) continue;
         const uint32_t n = a.sizes[g * kStreams + s];
         if (a.sizes[g * kStreams] == ~0u) continue;  // unsupported chunk
-        if (++epoch >= kTagEpochs) {  // tag space exhausted: clear the table once
-            for (uint32_t i = (uint32_t)lane; i < (1u << 13); i += 64) gst<uint4>(S.ht + 4 * i, make_uint4(0, 0, 0, 0));
-            epoch = 1;
-            wave_sync();
-        }
+        ht_next_epoch(S.ht, epoch, n);
         // VBZ: the svb16 buffer starts at the offset its split recorded in sizes[1]
         const uint8_t* src = a.streams + g * kChunkStreamBytes + (a.nu == 1 ? a.sizes[g * kStreams + 1] : stream_off(s));
         uint8_t* dst = a.frames + g * kChunkFrameBytes + frame_off(s);
-        const size_t fsz = zstd1_compress_wave(dst, src, n, S, epoch, P);
+        const size_t fsz = zstd1_compress_wave(dst, src, n, S, epoch & 0xFFu, P);
         if (lane == 0) a.fsizes[g * kStreams + s] = (uint32_t)fsz;
         wave_sync();
     }
@@ -638,7 +634,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
     S.huf = (uint32_t*)(sbase + lay.huf);
     uint8_t* streams = sbase + lay.bytes;
     uint8_t* fbuf = streams + kChunkStreamBytes;
-    uint32_t epoch = a.epochs[blockIdx.x];
+    uint32_t epoch = a.epochs[blockIdx.x];  // table state: epoch tag | written extent << 8 (ht_next_epoch)
     PhaseProf P;
     P.init(a.prof);
     while (true) {
@@ -705,15 +701,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
 #pragma unroll
         for (int s = 0; s < nf; s++) {
             if (s < nf - 1) off += 8;  // length prefixes of all frames but the last (C5.hpp:429-462)
-            if (++epoch >= kTagEpochs) {  // tag space exhausted: clear the table once
-                for (uint32_t i = (uint32_t)lane; i < (1u << 13); i += 64) gst<uint4>(S.ht + 4 * i, make_uint4(0, 0, 0, 0));
-                epoch = 1;
-                wave_sync();
-            }
+            ht_next_epoch(S.ht, epoch, sz[s]);
             // straight into the blob when the frame bound fits the capacity; otherwise through the
             // slot's frame buffer (the reference compresses into its own buffers, then checks)
             const bool direct = ok && off + frame_bound(sz[s]) <= cap;
-            const size_t f = uni(zstd1_compress_wave(direct ? dst + off : fbuf, src[s], sz[s], S, epoch, P));
+            const size_t f = uni(zstd1_compress_wave(direct ? dst + off : fbuf, src[s], sz[s], S, epoch & 0xFFu, P));
             wave_sync();
             if (!direct && ok) {
                 if (off + f <= cap) wave_copy(dst + off, fbuf, f);

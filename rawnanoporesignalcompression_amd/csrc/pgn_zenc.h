@@ -150,6 +150,24 @@ __device__ inline uint32_t ht_entry(uint32_t tag, uint32_t idx, uint32_t bytes, 
 {
     return (tag << kTagShift) | ht_fp(bytes, idxBits) | idx;
 }
+// A slot's table state between frames (kept in the kernels' epochs array across launches): the
+// epoch tag (low 8 bits) and the log2 extent of the entries written since the last clear (above).
+// Advances to the epoch of a frame of n bytes; when the tags run out, clears only that extent.
+__device__ __forceinline__ void ht_next_epoch(uint32_t* ht, uint32_t& st, uint32_t n)
+{
+    uint32_t ep = (st & 0xFFu) + 1u, dirty = st >> 8;
+    if (ep >= kTagEpochs) {
+        for (uint32_t i = (uint32_t)lane_id(); i < ((1u << dirty) >> 2); i += 64) gst<uint4>(ht + 4 * i, make_uint4(0, 0, 0, 0));
+        ep = 1;
+        dirty = 0;
+        wave_sync();
+    }
+    if (n >= 7) {  // smaller frames are raw blocks and write no entries
+        const uint32_t hl = z1::level1_params(n).hashLog;
+        dirty = hl > dirty ? hl : dirty;
+    }
+    st = ep | (dirty << 8);
+}
 
 // ZSTD_hashPtr (mls 5 / 6 / 7) over 8 global bytes
 __device__ __forceinline__ uint32_t hash_g(const uint8_t* p, unsigned hlog, unsigned mls)
