@@ -408,6 +408,11 @@ class Pod5SignalBatch:
         data = np.ascontiguousarray(data, dtype=np.uint8)
         samples = np.ascontiguousarray(samples, dtype=np.uint32)
         k = samples.size
+        # pgn_pod5_decompress_rows reads offsets[k] and the bytes offsets[0] .. offsets[k]
+        if offsets.size != k + 1:
+            raise ValueError(f"offsets has {offsets.size} entries, expected rows + 1 = {k + 1}")
+        if k and (int(offsets[-1]) > data.size or np.any(np.diff(offsets.astype(np.int64)) < 0)):
+            raise ValueError("offsets are not monotonic or run past the data buffer")
         out = np.empty(max(int(samples.sum()), 1), dtype=np.int16)
         st = np.zeros(max(k, 1), dtype=np.int32)
         _check(self._lib.pgn_pod5_decompress_rows(self._h, k, offsets.ctypes.data, data.ctypes.data if data.size else None,

@@ -84,8 +84,12 @@ __host__ __device__ inline EncLayout enc_layout()
 }
 
 struct DecLayout {
-    size_t lit, seqs, tables, htab, bytes;
+    size_t lit, seqs, tables, htab, seg, bytes;
 };
+// segment regions of the one-pass Huffman decoder: (all literal bits) / (shortest code) bytes, so a
+// full 128 KiB block whose average code is up to 2.5x its shortest (a wider one decodes one lane per
+// stream straight into place)
+constexpr size_t kSegScratch = (size_t)320 << 10;
 __host__ __device__ inline DecLayout dec_layout()
 {
     DecLayout l{};
@@ -95,6 +99,7 @@ __host__ __device__ inline DecLayout dec_layout()
     l.seqs = take(12 * (size_t)kMaxDecSeq);
     l.tables = take(4 * ((size_t)kSeqTab + 4));
     l.htab = take(2u << z1::kHufTableLogMax);
+    l.seg = take(kSegScratch);
     l.bytes = o;
     return l;
 }
@@ -276,6 +281,7 @@ struct DecArgs {
     uint64_t* prof;
     size_t base, G;
     uint32_t nu;         // zstd work units per chunk: 5 (C5) or 1 (VBZ)
+    uint32_t segCap;     // Huffman segment scratch per slot; 0 = the two-pass decoder (PGN_HUF=twopass)
 };
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
@@ -330,6 +336,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     S.maxSeq = kMaxDecSeq;
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
+    S.seg = sbase + lay.seg;
+    S.segCap = a.segCap;
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = (size_t)a.nu * G;
@@ -791,6 +799,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.maxSeq = kMaxDecSeq;
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
+    S.seg = sbase + lay.seg;
+    S.segCap = a.segCap;
     uint8_t* inter = sbase + lay.bytes;
     PhaseProf P;
     P.init(a.prof);
@@ -951,6 +961,7 @@ struct pgn_ctx {
     size_t encStagedBelow = 0;
     size_t encFusedSlotsMax = 0, decFusedSlotsMax = 0;
     size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH, staged pipeline)
+    uint32_t hufSegCap = 0;  // the one-pass Huffman decoder (PGN_HUF=seg) or the two-pass one (0, default)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
@@ -1066,6 +1077,7 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         c->encForced = true;
     }
     if (const char* pp = getenv("PGN_DEC_PIPELINE")) c->decStaged = strcmp(pp, "staged") == 0;
+    if (const char* h = getenv("PGN_HUF")) c->hufSegCap = strcmp(h, "seg") == 0 ? (uint32_t)kSegScratch : 0u;
     if (const char* sb = getenv("PGN_SUBBATCH")) {
         long v = atol(sb);
         if (v > 0) c->subBatch = (size_t)v;
@@ -1261,6 +1273,7 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     a.slotBytes = dec_slot_bytes();
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.queue = c->queues;
+    a.segCap = c->hufSegCap;
     c->lastUnits = nullptr;
     switch (codec) {
     case kCodecC5: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
@@ -1383,6 +1396,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.G = G;
     a.nu = nu;
+    a.segCap = c->hufSegCap;
     // pass p: parse + zstd on the caller's stream into buffer p % 2, merge on the side stream.  The
     // merge of pass p overlaps the zstd kernel of pass p+1; a buffer is parsed into again only after
     // the merge of the pass before last has read it.

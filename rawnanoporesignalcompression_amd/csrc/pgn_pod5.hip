@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <new>
+#include <stdexcept>
 #include <vector>
 
 #include "../../include/pgnano_pod5.h"
@@ -17,8 +19,10 @@
 
 namespace {
 
-// exclusive scan of sizes[0..n) -> offs[0..n], offs[n] = total; first[0] = index of the first
-// non-OK status (n if none).  One workgroup of 1024 threads, tiles of 1024 with a running carry.
+// exclusive scan of the sizes of the chunks that succeeded (a failed chunk counts 0: the multi-frame
+// encoders report the reference's "Required size" there, which may exceed the chunk's capacity)
+// -> offs[0..n], offs[n] = total; first[0] = index of the first non-OK status (n if none).  One
+// workgroup of 1024 threads, tiles of 1024 with a running carry.
 __global__ __launch_bounds__(1024) void pod5_scan_kernel(const uint64_t* sizes, const int32_t* status, uint64_t* offs,
                                                          uint32_t* first, uint32_t n)
 {
@@ -33,8 +37,9 @@ __global__ __launch_bounds__(1024) void pod5_scan_kernel(const uint64_t* sizes, 
     __syncthreads();
     for (uint32_t base = 0; base < n; base += 1024) {
         const uint32_t i = base + t;
-        const uint64_t v = i < n ? sizes[i] : 0;
-        if (i < n && status[i] != 0) atomicMin(&bad, i);
+        const bool ok = i < n && status[i] == 0;
+        const uint64_t v = ok ? sizes[i] : 0;
+        if (i < n && !ok) atomicMin(&bad, i);
         s[t] = v;
         __syncthreads();
         for (uint32_t d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
@@ -352,8 +357,29 @@ int pgn_pod5_decompress_rows(pgn_pod5_batch* b, uint32_t row_count, const uint64
 // pgnano_pod5file.h: `copy --pgnano | --VBZ` of a file's signal table.  Device-resident between the
 // two launches: blobs up -> batched decode into one sample buffer -> batched encode -> device-side
 // pack -> packed blobs down.
+static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
+                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats);
+
+// the host vectors are sized from the file: an allocation failure (or any exception) becomes a
+// status instead of crossing the C ABI
 int pgn_pod5_transcode_file(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
                             int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats)
+{
+    try {
+        return transcode_impl(ctx, in_path, out_path, dst_signal_type, pgnano_variant, rows_per_batch, stats);
+    } catch (const std::bad_alloc&) {
+        snprintf(g_pod5_err, sizeof(g_pod5_err), "out of host memory");
+        return PGN_ERR_IO;
+    } catch (const std::exception& e) {
+        snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", e.what());
+        return PGN_ERR_CORRUPT;
+    }
+}
+
+}  // extern "C"
+
+static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
+                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats)
 {
     if (!ctx || !in_path || !out_path || dst_signal_type < PGN_POD5_SIGNAL_UNCOMPRESSED ||
         dst_signal_type > PGN_POD5_SIGNAL_PGNANO || pgnano_variant < PGN_VARIANT_C5 || pgnano_variant > PGN_VARIANT_VBZ0)
@@ -506,4 +532,4 @@ int pgn_pod5_transcode_file(pgn_ctx* ctx, const char* in_path, const char* out_p
     return rc;
 }
 
-}  // extern "C"
+

@@ -495,8 +495,10 @@ void parse_signal_table(pgn_pod5_file& f, size_t base, size_t len)
     for (uint32_t i = 0; i < bv.len; i++) {
         Block blk;
         memcpy(&blk, footer.p + bv.start + (size_t)i * sizeof(Block), sizeof(Block));
-        if (blk.offset < 8 || blk.meta_len < 8 || blk.body_len < 0 || (uint64_t)blk.offset + blk.meta_len > len ||
-            (uint64_t)blk.offset + blk.meta_len + (uint64_t)blk.body_len > len)
+        // compared without sums, so that values near INT64_MAX cannot wrap past the checks
+        if (blk.offset < 8 || blk.meta_len < 8 || blk.body_len < 0 || (uint64_t)blk.offset > len ||
+            (uint64_t)blk.meta_len > len - (uint64_t)blk.offset ||
+            (uint64_t)blk.body_len > len - (uint64_t)blk.offset - (uint64_t)blk.meta_len)
             corrupt("Arrow record batch block out of range");
         const uint8_t* m = a + blk.offset;
         uint32_t cont;
@@ -527,11 +529,14 @@ void parse_signal_table(pgn_pod5_file& f, size_t base, size_t len)
         auto buf = [&](size_t k, int64_t need) {
             ArrowBuf bb;
             memcpy(&bb, mb.p + bufv.start + 16 * k, 16);
-            if (bb.offset < 0 || bb.length < need || bb.offset + bb.length > blk.body_len)
+            if (bb.offset < 0 || bb.length < 0 || bb.offset > blk.body_len || bb.length > blk.body_len - bb.offset ||
+                bb.length < need)
                 corrupt("Arrow buffer out of range");
             return std::make_pair(body + bb.offset, bb.length);
         };
-        if (length < 0) corrupt("negative batch length");
+        // 16 bytes of read id per row: any larger length cannot fit the body (and 16 * length
+        // below cannot overflow)
+        if (length < 0 || length > blk.body_len / 16) corrupt("batch length out of range");
         for (int c = 0; c < 3; c++) {
             const auto nd = node(firstNode[c]);
             if (nd.first != length) corrupt("Arrow field length differs from the batch length");

@@ -72,6 +72,8 @@ struct DecScratch {
     uint32_t maxSeq;
     uint32_t* tables;       // the three sequence FSE tables of a multi-block frame (kSeqTab + 4 words)
     uint16_t* htab;         // 4096 entries: a 12-bit Huffman table, or the parked LDS table
+    uint8_t* seg;           // segment regions of the one-pass Huffman decoder (pgn_hufseg.h)
+    uint32_t segCap;        // their bytes; 0 selects the two-pass decoder (pgn_huf4.h)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -321,9 +323,10 @@ __device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxS
     return true;
 }
 
-// Returns header bytes consumed (0 = corrupt); *tlOut = table log.  Fills sDec.tab, or gt (4096
-// entries in HBM) for a 12-bit table.
-__device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt)
+// Returns header bytes consumed (0 = corrupt); *tlOut = table log, *minNbOut = its shortest code.
+// Fills sDec.tab, or gt (4096 entries in HBM) for a 12-bit table.
+__device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
+                                                     unsigned* minNbOut)
 {
     const int lane = lane_id();
     src = uni(src);
@@ -495,13 +498,19 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
         }
     }
     lds_sync();
+    uint32_t wmax = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) wmax = w4[q] > wmax ? w4[q] : wmax;
+    wmax = wave_max(wmax);
     *tlOut = tl;
+    *minNbOut = tl + 1 - wmax;
     return used;
 }
 
 }  // namespace pgn
 
 #include "pgn_huf4.h"
+#include "pgn_hufseg.h"
 
 namespace pgn {
 
@@ -863,6 +872,8 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
     S.htab = uni(S.htab);
+    S.seg = uni(S.seg);
+    S.segCap = uni(S.segCap);
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
     HdrWin hw;
@@ -903,7 +914,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
         bool hufValid = false;  // a Huffman table exists for treeless literals
         bool hufInLds = false;  // ... and is in sDec.tab (tables up to kHufLdsLog)
         bool hufParked = false; // ... and a copy is parked in S.htab
-        unsigned hufTl = 0;
+        unsigned hufTl = 0, hufMinNb = 1;
         SeqState fs;  // frame state of the sequences stage: repeat offsets, table validity
         while (true) {
             if (srcSize - ip < 3) return z1::kDecErrSrcSmall;
@@ -971,13 +982,14 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     const uint8_t* hp = blk + lh;
                     size_t remain = cs;
                     if (ltype == z1::kSetCompressed) {
-                        unsigned tlNew = 0;
-                        const size_t hsz = huf_build_dtable_wave(hp, remain, &tlNew, S.htab);
+                        unsigned tlNew = 0, mnNew = 1;
+                        const size_t hsz = huf_build_dtable_wave(hp, remain, &tlNew, S.htab, &mnNew);
                         P.count(9);
                         P.mark(1);
                         if (hsz == 0) return z1::kDecErrHufTable;
                         hufValid = true;
                         hufTl = tlNew;
+                        hufMinNb = mnNew;
                         hufInLds = tlNew <= kHufLdsLog;
                         hufParked = !hufInLds;
                         hp += hsz;
@@ -1000,9 +1012,13 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                             ok = false;
                         } else {
                             const size_t jp = (size_t)(hp - src);  // the jump table, from the header window
-                            ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs,
-                                                  hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16),
-                                                  hw_u16(hw, src, jp + 4), P);
+                            const uint32_t jt01 = hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16);
+                            const uint32_t jt2 = hw_u16(hw, src, jp + 4);
+                            if (S.segCap)
+                                ok = huf_seg_decode4_wave(hufTl, hufMinNb, hp, remain, litOut, (uint32_t)rs, jt01, jt2,
+                                                          S.seg, S.segCap, P);
+                            else
+                                ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, P);
                         }
                     }
                     if (ballot(!ok)) return z1::kDecErrHufStream;

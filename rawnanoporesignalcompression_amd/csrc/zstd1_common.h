@@ -9,6 +9,9 @@
 // These functions are the serial pieces that both the host model (zstd1_model.hip, test-only) and
 // the GPU kernels (pgn_kernels.hip) run; the GPU replaces the data-parallel stages (match search,
 // histograms, Huffman bit packing) with wave-parallel code of identical output.
+//
+// Parts of this file restate algorithms of Zstandard (libzstd 1.4.x), Copyright (c) 2016-present,
+// Facebook, Inc., used under its BSD licence: see THIRD_PARTY_NOTICES.md at the repository root.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>

@@ -6,6 +6,9 @@
 // Scope: everything ZSTD_decompress accepts without a dictionary -- concatenated and skippable
 // frames, raw / RLE / compressed blocks, raw / RLE / Huffman / treeless literals, predefined / RLE /
 // FSE / repeat sequence tables, repeat offsets, optional content checksum (skipped).
+//
+// Parts of this file restate algorithms of Zstandard (libzstd 1.4.x), Copyright (c) 2016-present,
+// Facebook, Inc., used under its BSD licence: see THIRD_PARTY_NOTICES.md at the repository root.
 #pragma once
 #include "zstd1_common.h"
 

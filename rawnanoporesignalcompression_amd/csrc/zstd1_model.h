@@ -3,6 +3,9 @@
 //
 // Host and device: the GPU kernels run the serial parts of these on one lane; the host build
 // (libpgn_model.so, test-only) lets the test-suite fuzz the exact same code against libzstd.
+//
+// Parts of this file restate algorithms of Zstandard (libzstd 1.4.x), Copyright (c) 2016-present,
+// Facebook, Inc., used under its BSD licence: see THIRD_PARTY_NOTICES.md at the repository root.
 #pragma once
 #include "zstd1_common.h"
 

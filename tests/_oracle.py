@@ -246,7 +246,9 @@ def oracle_vbz_svb_encode(x: np.ndarray) -> bytes:
 
 # ------------------------------------------------------------------------------------------------
 # The reference's own svb16 stages, compiled verbatim from /root/reference by oracle/ref.mk into
-# oracle/_ref/ (absent on the GPU box and wherever /root/reference is not mounted: ref() is then None).
+# oracle/_ref/.  They are used only where the reference tree itself is present (this container):
+# ref() is None elsewhere, so GPU-box test processes never load them, whether or not the built
+# libraries travelled with the tree.
 # ------------------------------------------------------------------------------------------------
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libpgn_ref.so")
 REF_VBZ_SO = os.path.join(ROOT, "oracle", "_ref", "libpgn_ref_vbz.so")
@@ -255,14 +257,18 @@ _r = None
 _rv = None
 
 
+def ref_available() -> bool:
+    return os.path.exists(REF_SRC)
+
+
 def ref():
-    """libpgn_ref.so (the reference's svb16 split/merge of every variant), built when the reference tree
-    is present; None when neither the library nor the reference sources exist."""
+    """libpgn_ref.so (the reference's svb16 split/merge of every variant), built from the reference tree;
+    None where the reference sources are absent."""
     global _r, _rv
     if _r is None:
+        if not ref_available():
+            return None
         if not (os.path.exists(REF_SO) and os.path.exists(REF_VBZ_SO)):
-            if not os.path.exists(REF_SRC):
-                return None
             subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-f", "ref.mk"], check=True,
                            capture_output=True)
         L = C.CDLL(REF_SO)

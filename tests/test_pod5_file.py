@@ -250,3 +250,64 @@ def test_fixture_digest_unchanged():
     if os.path.exists(ref):
         assert hashlib.sha256(open(ref, "rb").read()).hexdigest() == h
     assert os.path.getsize(FIXTURE) == 1_323_624
+
+
+def _signal_arrow_fields(raw: bytes):
+    """Byte positions (in the file) of the signal table's first record-batch Block struct, of its
+    RecordBatch length and of its Buffer structs, found with the independent flatbuffer reader above
+    (Arrow File.fbs: Footer.recordBatches = field 3; Message.header = field 2; RecordBatch: length =
+    field 0, buffers = field 2)."""
+    foot = parse_footer(raw)
+    off, ln = next((o, l) for o, l, _, ctype in foot["files"] if ctype == 1)  # ContentType.SignalTable
+    t = raw[off:off + ln]
+    flen = struct.unpack_from("<i", t, len(t) - 10)[0]
+    fstart = len(t) - 10 - flen
+    fb = t[fstart:fstart + flen]
+    root = fb_table(fb, struct.unpack_from("<I", fb, 0)[0])
+    f = fb_field(root, 3)
+    v = f + struct.unpack_from("<I", fb, f)[0]
+    block = off + fstart + v + 4  # first Block {int64 offset, int32 metaDataLength, pad, int64 bodyLength}
+    boff, mlen = struct.unpack_from("<qi", t, fstart + v + 4)
+    m = boff + 8  # continuation marker + length, then the Message flatbuffer
+    msg = fb_table(t[m:], struct.unpack_from("<I", t, m)[0])
+    h = fb_field(msg, 2)
+    rb = fb_table(t[m:], h + struct.unpack_from("<I", t, m + h)[0])
+    length = off + m + fb_field(rb, 0)
+    bf = fb_field(rb, 2)
+    bv = bf + struct.unpack_from("<I", t, m + bf)[0]
+    nbuf = struct.unpack_from("<I", t, m + bv)[0]
+    buffers = [off + m + bv + 4 + 16 * i for i in range(nbuf)]
+    return block, length, buffers
+
+
+def test_int64_extreme_arrow_fields_fail_with_status(tmp_path):
+    """Offsets and lengths near INT64_MAX in the Arrow block, record batch and buffer fields are
+    rejected (the checks compare without sums that could wrap)."""
+    from rawnanoporesignalcompression_amd import _native
+
+    Pm = P()
+    raw = open(FIXTURE, "rb").read()
+    block, length, buffers = _signal_arrow_fields(raw)
+    assert struct.unpack_from("<q", raw, length)[0] > 0
+    big = (1 << 63) - 1
+    edits = {
+        "block_offset": [(block, "<q", big - 4)],
+        "block_body": [(block + 16, "<q", big - 16)],
+        "batch_length": [(length, "<q", 1 << 62)],
+        "batch_length_wrap": [(length, "<q", (1 << 60) + 1)],
+    }
+    # the buffers the reader dereferences (the validity bitmaps are empty and never read)
+    for i, b in enumerate(b for b in buffers[:8] if struct.unpack_from("<q", raw, b + 8)[0] > 0):
+        edits[f"buf{i}_offset"] = [(b, "<q", big - 8)]
+        edits[f"buf{i}_length"] = [(b + 8, "<q", big)]
+        edits[f"buf{i}_both"] = [(b, "<q", 1 << 62), (b + 8, "<q", 1 << 62)]
+    for name, ed in edits.items():
+        blob = bytearray(raw)
+        for pos, fmt, val in ed:
+            struct.pack_into(fmt, blob, pos, val)
+        p = tmp_path / f"{name}.pod5"
+        p.write_bytes(bytes(blob))
+        with pytest.raises(Pm.Pod5FileError) as e:
+            with Pm.Pod5File(str(p)) as f:
+                f.signal_table()
+        assert e.value.status in (_native.PGN_ERR_CORRUPT, _native.PGN_ERR_UNSUPPORTED), name

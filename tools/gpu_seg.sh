@@ -1,0 +1,16 @@
+#!/bin/bash
+# One-pass segmented Huffman decoder vs the two-pass one (run via gpurun): GPU tests on the default
+# (segmented) decoder, codec timing A/B, phase profile of both.
+TAG=${1:-seg}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+PGN_HUF=seg timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1
+rc=$?; tail -3 gpurun_out/gpu_tests_$TAG.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/gpu_tests_$TAG.log | head -20; exit $rc; }
+for H in twopass seg twopass seg; do
+  PGN_HUF=$H timeout -k 10 120 python3 tools/codec_timing.py 30000 3 > gpurun_out/timing_${TAG}_$H.log 2>&1 || exit 1
+  echo "$H: $(tail -1 gpurun_out/timing_${TAG}_$H.log)"
+done
+for H in twopass seg; do
+  PGN_HUF=$H timeout -k 10 200 python -u tools/phase_profile.py 20000 > gpurun_out/phase_${TAG}_$H.log 2>&1 || exit 1
+  echo "== $H"; sed -n '/^decode:/,$p' gpurun_out/phase_${TAG}_$H.log | head -32
+done
