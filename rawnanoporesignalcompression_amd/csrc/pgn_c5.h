@@ -291,6 +291,8 @@ struct MergeLds {
     // A step has at most 1024 of them together, plus the alignment slack of two windows.
     alignas(16) uint16_t V[1024 + 64 + 32 + 32];
     uint16_t zero[2];  // what a class-0 sample reads
+    // S byte -> its two entries (low nibble first), offset added and zig-zag decoded
+    alignas(16) uint32_t nib[256];
 };
 
 // stage bytes [a, a + len) of `in` (len <= cap - 15) into W; returns the window's first address
@@ -393,78 +395,143 @@ __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, uint3
     }
 }
 
+// One step's bookkeeping, computed a step ahead: the key word, the class counts below this lane,
+// the step's totals and the staging ranges of its S / M / class-3 bytes.
+struct MergePlan {
+    uint32_t kw;
+    uint32_t excl;        // classes 1 | 2 << 11 | 3 << 22 of the lanes below (exact: at most 1008 each)
+    uint32_t ns, nm, nl;  // the step's class counts
+    uint64_t aS, aS0, aM, aM0;
+    uint32_t nbS, nbM;
+};
+
 template <bool C4 = false>
 __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
                                              uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint64_t* consumed,
                                              MergeLds& W)
 {
+    using CO = ClassOffsets<C4>;
     const uint32_t lane = (uint32_t)lane_id();
     const uint64_t kl = ((uint64_t)n + 3) / 4;
     const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
     uint64_t sN = 0, mN = 0, lN = 0;  // nibbles / bytes consumed so far (wave-uniform)
     uint32_t carry = 0;
     if (lane == 0) W.zero[0] = 0;
-    for (uint32_t t = 0; t < n; t += kSplitStep) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // the S table: byte -> two entries
+        const uint32_t bt = 4 * lane + q;
+        W.nib[bt] = (uint32_t)zz_dec16((uint16_t)((bt & 15u) + CO::o1)) |
+                    ((uint32_t)zz_dec16((uint16_t)((bt >> 4) + CO::o1)) << 16);
+    }
+    // the key word of the step at t (codes past the signal's end are not samples)
+    auto key_word = [&](uint32_t t) -> uint32_t {
         const bool full = t + kSplitStep <= n;
         const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
         const uint64_t kb0 = t >> 2;
-        if (kb0 + nK > total) return 1;
         uint32_t kw = 0;
         if (4u * lane + 4u <= nK) {
             kw = ld32u(in + kb0 + 4u * lane);
         } else {
             for (uint32_t b = 4u * lane; b < nK; b++) kw |= (uint32_t)gb(in + kb0 + b) << (8u * (b - 4u * lane));
         }
-        if (!full) {  // codes past the end of the signal are not samples
+        if (!full) {
             const uint32_t first = 16u * lane, nv = (n - t) > first ? (n - t) - first : 0u;
             if (nv < 16) kw &= (1u << (2u * nv)) - 1u;
         }
-        // class counts of my 16 samples, their lane prefix and the step totals
+        return kw;
+    };
+    // the plan of step t from its key word; false if the step reads past `total` (the reference's UB)
+    auto plan = [&](uint32_t t, uint32_t kw, MergePlan& pn) -> bool {
+        const uint32_t nK = t + kSplitStep <= n ? kSplitStep / 4 : (n - t + 3) / 4;
+        if ((t >> 2) + nK > total) return false;
         const uint32_t lo = kw & 0x55555555u, hi = (kw >> 1) & 0x55555555u;
-        const uint32_t n1 = (uint32_t)__builtin_popcount(lo & ~hi), n2 = (uint32_t)__builtin_popcount(hi & ~lo);
-        const uint32_t n3 = (uint32_t)__builtin_popcount(lo & hi);
-        const uint32_t p12 = n1 | (n2 << 16);
-        const uint32_t i12 = wave_incl_sum(p12), i3 = wave_incl_sum(n3);
-        const uint32_t t12 = readlane_u32(i12, 63);
-        const uint32_t ns = t12 & 0xFFFFu, nm = t12 >> 16, nl = readlane_u32(i3, 63);
-        if (ps + ((sN + ns + 1) >> 1) > total || pm + mN + nm > total || pl + lN + nl > total || ph + lN + nl > total)
-            return 1;
-        // stage the step's values: S blocks, then M blocks, then the class-3 values, into one window;
-        // the first 64 blocks of each and 64 class-3 values are loaded together
-        const uint64_t aS = ps + (sN >> 1), aS0 = aS & ~(uint64_t)15;
-        const uint32_t nbS = (uint32_t)((ps + ((sN + ns + 1) >> 1) - aS0 + 15) >> 4);
-        const uint64_t aM = pm + mN, aM0 = aM & ~(uint64_t)15;
-        const uint32_t nbM = (uint32_t)((aM + nm - aM0 + 15) >> 4);
-        const uint32_t eM = 32u * nbS, eL = eM + 16u * nbM;  // entry offsets of the M and class-3 windows
+        const uint32_t pc = (uint32_t)__builtin_popcount(lo & ~hi) | ((uint32_t)__builtin_popcount(hi & ~lo) << 11) |
+                            ((uint32_t)__builtin_popcount(lo & hi) << 22);
+        const uint32_t inc = wave_incl_sum(pc);
+        pn.kw = kw;
+        pn.excl = inc - pc;
+        // field 3 has 10 bits: rebuild its total from the last lane (the split's wrap rule)
+        const uint32_t e63 = readlane_u32(pn.excl, 63), p63 = readlane_u32(pc, 63);
+        const uint32_t t12 = readlane_u32(inc, 63);
+        pn.ns = t12 & 0x7FFu;
+        pn.nm = (t12 >> 11) & 0x7FFu;
+        pn.nl = (e63 >> 22) + (p63 >> 22);
+        if (ps + ((sN + pn.ns + 1) >> 1) > total || pm + mN + pn.nm > total || pl + lN + pn.nl > total ||
+            ph + lN + pn.nl > total)
+            return false;
+        pn.aS = ps + (sN >> 1);
+        pn.aS0 = pn.aS & ~(uint64_t)15;
+        pn.nbS = (uint32_t)((ps + ((sN + pn.ns + 1) >> 1) - pn.aS0 + 15) >> 4);
+        pn.aM = pm + mN;
+        pn.aM0 = pn.aM & ~(uint64_t)15;
+        pn.nbM = (uint32_t)((pn.aM + pn.nm - pn.aM0 + 15) >> 4);
+        return true;
+    };
+    if (n == 0) {
+        *consumed = ph;
+        return 0;
+    }
+    // prologue: step 0's plan and staged bytes, step 1's key word
+    MergePlan cur;
+    if (!plan(0, key_word(0), cur)) return 1;
+    uint32_t kwNext = kSplitStep < n ? key_word(kSplitStep) : 0u;
+    uint4 vS = make_uint4(0, 0, 0, 0), vM = vS;
+    uint32_t lb = 0, hb = 0;
+    auto load_stage = [&](const MergePlan& pn) {
+        if (lane < pn.nbS) vS = gld<uint4>(in + pn.aS0 + 16u * lane);
+        if (lane < pn.nbM) vM = gld<uint4>(in + pn.aM0 + 16u * lane);
+        if (lane < pn.nl) {
+            lb = gb(in + pl + lN + lane);
+            hb = gb(in + ph + lN + lane);
+        }
+    };
+    load_stage(cur);
+    lds_sync();
+    for (uint32_t t = 0; t < n; t += kSplitStep) {
+        const bool full = t + kSplitStep <= n;
+        // ---- this step's bytes into the window (loaded a step ago): S by table, M and class 3 by arithmetic
+        const uint32_t eM = 32u * cur.nbS, eL = eM + 16u * cur.nbM;
         {
-            constexpr uint32_t add1 = ClassOffsets<C4>::o1 * 0x00010001u, add2 = ClassOffsets<C4>::o2 * 0x00010001u;
-            uint4 vS = make_uint4(0, 0, 0, 0), vM = vS;
-            uint32_t lb = 0, hb = 0;
-            if (lane < nbS) vS = gld<uint4>(in + aS0 + 16u * lane);
-            if (lane < nbM) vM = gld<uint4>(in + aM0 + 16u * lane);
-            if (lane < nl) {
-                lb = gb(in + pl + lN + lane);
-                hb = gb(in + ph + lN + lane);
+            constexpr uint32_t add2 = CO::o2 * 0x00010001u;
+            if (lane < cur.nbS) {
+                const uint32_t w[4] = {vS.x, vS.y, vS.z, vS.w};
+                uint32_t o[16];
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) o[4 * j + k] = W.nib[(w[j] >> (8 * k)) & 0xFFu];
+                uint4* q = (uint4*)(W.V + 32u * lane);
+                q[0] = make_uint4(o[0], o[1], o[2], o[3]);
+                q[1] = make_uint4(o[4], o[5], o[6], o[7]);
+                q[2] = make_uint4(o[8], o[9], o[10], o[11]);
+                q[3] = make_uint4(o[12], o[13], o[14], o[15]);
             }
-            if (lane < nbS) put_nibbles16(W.V + 32u * lane, vS, add1);
-            if (lane < nbM) put_bytes16(W.V + eM + 16u * lane, vM, add2);
-            if (lane < nl) W.V[eL + lane] = zz_dec16((uint16_t)((lb | (hb << 8)) + ClassOffsets<C4>::o3));
-            for (uint32_t b = lane + 64; b < nbS; b += 64) put_nibbles16(W.V + 32u * b, gld<uint4>(in + aS0 + 16u * b), add1);
-            for (uint32_t b = lane + 64; b < nbM; b += 64) put_bytes16(W.V + eM + 16u * b, gld<uint4>(in + aM0 + 16u * b), add2);
-            for (uint32_t i = lane + 64; i < nl; i += 64)
-                W.V[eL + i] = zz_dec16((uint16_t)(((uint32_t)gb(in + pl + lN + i) | ((uint32_t)gb(in + ph + lN + i) << 8)) + ClassOffsets<C4>::o3));
+            if (lane < cur.nbM) put_bytes16(W.V + eM + 16u * lane, vM, add2);
+            if (lane < cur.nl) W.V[eL + lane] = zz_dec16((uint16_t)((lb | (hb << 8)) + CO::o3));
+            for (uint32_t b = lane + 64; b < cur.nbS; b += 64) put_nibbles16(W.V + 32u * b, gld<uint4>(in + cur.aS0 + 16u * b), CO::o1 * 0x00010001u);
+            for (uint32_t b = lane + 64; b < cur.nbM; b += 64) put_bytes16(W.V + eM + 16u * b, gld<uint4>(in + cur.aM0 + 16u * b), add2);
+            for (uint32_t i = lane + 64; i < cur.nl; i += 64)
+                W.V[eL + i] = zz_dec16((uint16_t)(((uint32_t)gb(in + pl + lN + i) | ((uint32_t)gb(in + ph + lN + i) << 8)) + CO::o3));
         }
         lds_sync();
         // LDS byte places of my first value of each class
         constexpr uint32_t offV = (uint32_t)__builtin_offsetof(MergeLds, V);
-        const uint32_t e12 = i12 - p12;
-        const uint32_t pS = offV + 2u * ((uint32_t)(2 * (aS - aS0) + (sN & 1)) + (e12 & 0xFFFFu));
-        const uint32_t pM = offV + 2u * (eM + (uint32_t)(aM - aM0) + (e12 >> 16));
-        const uint32_t pL = offV + 2u * (eL + (i3 - n3));
+        const uint32_t pS = offV + 2u * ((uint32_t)(2 * (cur.aS - cur.aS0) + (sN & 1)) + (cur.excl & 0x7FFu));
+        const uint32_t pM = offV + 2u * (eM + (uint32_t)(cur.aM - cur.aM0) + ((cur.excl >> 11) & 0x7FFu));
+        const uint32_t pL = offV + 2u * (eL + (cur.excl >> 22));
+        const uint32_t kw = cur.kw;
+        sN += cur.ns;
+        mN += cur.nm;
+        lN += cur.nl;
+        // ---- the next step: its plan (key word loaded a step ago), its bytes in flight during this merge
+        const uint32_t tn = t + kSplitStep;
+        bool more = tn < n;
+        if (more) {
+            if (!plan(tn, kwNext, cur)) return 1;
+            if (tn + kSplitStep < n) kwNext = key_word(tn + kSplitStep);
+            load_stage(cur);
+        }
         merge_step(W, kw, pS, pM, pL, carry, out, t, n, full);
-        sN += ns;
-        mN += nm;
-        lN += nl;
         lds_sync();
     }
     *consumed = ph + lN;

@@ -28,9 +28,9 @@ namespace pgn {
 
 constexpr int kSegMax = 16;              // segments (lanes) per stream
 constexpr int32_t kSegOv = 128;          // speculative overlap decoded above a segment's top
-constexpr int32_t kSegRec = 256;         // codeword starts recorded below a segment's top (sync window)
+constexpr int32_t kSegRec = 128;         // codeword starts recorded below a segment's top (sync window)
 constexpr int32_t kSegMinBits = 1536;    // shortest segment worth a lane of its own
-constexpr int32_t kSegStride = 10;       // window words consumed per round
+constexpr int32_t kSegStride = 8;        // window words consumed per round (the half that is restaged)
 constexpr int kSegMaxEpochs = kSegMax + 2;
 
 // ---------------------------------------------------------------------------------------------
@@ -48,39 +48,60 @@ struct SegRd {
     int32_t wb;
 };
 
-// words [wb, wb + 16) of base, bytes outside [off, end) read as zero (the stream's two ends: byte
-// loads, one 16-byte piece at a time)
-__device__ __forceinline__ void seg_fetch(const SegRd& r, int32_t wb, uint4 pf[4])
+// words [w, w + 4) of base (w % 4 == 0: one aligned 16-byte piece), bytes outside the stream
+// [off, end) read as zero.  A piece that holds any stream byte is loaded whole (it lies in the same
+// 16-byte block, so in the same page, as that byte) and the outside bytes are masked off; a piece
+// with none is not loaded.  Branch-free, so the prefetch of a round never waits on anything.
+__device__ __forceinline__ uint32_t seg_keep(int32_t lo, int32_t hi, int32_t i)  // bytes [lo, hi) of dword i
 {
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int32_t b = 4 * (wb + 4 * i);
-        if (b >= r.off && b + 16 <= r.end) {
-            pf[i] = gld<uint4>(r.base + b);
-        } else {
-            uint32_t v[4] = {0, 0, 0, 0};
-#pragma unroll 1
-            for (int t = 0; t < 16; t++) {
-                const int32_t x = b + t;
-                if (x >= r.off && x < r.end) v[t >> 2] |= (uint32_t)gb(r.base + x) << (8 * (t & 3));
-            }
-            pf[i] = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-    }
+    const int32_t a = lo - 4 * i, z = hi - 4 * i;  // keep bytes a .. z-1 of this dword
+    const uint32_t ma = a <= 0 ? ~0u : (a >= 4 ? 0u : (~0u << (8 * a)));
+    const uint32_t mz = z >= 4 ? ~0u : (z <= 0 ? 0u : (~0u >> (32 - 8 * z)));
+    return ma & mz;
 }
-// the window [wb, wb + 16) into the lane's ring column
-__device__ __forceinline__ void seg_stage(int32_t wb, const uint4 pf[4], int lane)
+__device__ __forceinline__ uint4 seg_load4(const SegRd& r, int32_t w)
 {
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        sDec.stg[(wb + 4 * i) & 15][lane] = pf[i].x;
-        sDec.stg[(wb + 4 * i + 1) & 15][lane] = pf[i].y;
-        sDec.stg[(wb + 4 * i + 2) & 15][lane] = pf[i].z;
-        sDec.stg[(wb + 4 * i + 3) & 15][lane] = pf[i].w;
+    const int32_t b = 4 * w;
+    if (b + 16 <= r.off || b >= r.end) return make_uint4(0u, 0u, 0u, 0u);
+    uint4 v = gld<uint4>(r.base + b);
+    if (b < r.off || b + 16 > r.end) {
+        const int32_t lo = r.off - b, hi = r.end - b;
+        v.x &= seg_keep(lo, hi, 0);
+        v.y &= seg_keep(lo, hi, 1);
+        v.z &= seg_keep(lo, hi, 2);
+        v.w &= seg_keep(lo, hi, 3);
     }
+    return v;
 }
-// the first window of a reader at P: words (P/32 - 14) .. (P/32 + 1)
-__device__ __forceinline__ int32_t seg_first_wb(int32_t P) { return (P >> 5) - 14; }
+// the prefetch form: pieces wholly inside or outside the stream only; a piece across the stream's
+// first byte (once per lane and stream) is left to seg_load4 at staging time (*edge set), so that no
+// wait follows the prefetch's loads
+__device__ __forceinline__ uint4 seg_prefetch4(const SegRd& r, int32_t w, bool& edge)
+{
+    const int32_t b = 4 * w;
+    const bool out = b + 16 <= r.off || b >= r.end, in = b >= r.off && b + 16 <= r.end;
+    edge = !out && !in;
+    return in ? gld<uint4>(r.base + b) : make_uint4(0u, 0u, 0u, 0u);
+}
+// words [w, w + 4) into the lane's ring column (slots w & 15 .. (w + 3) & 15; w % 4 == 0)
+__device__ __forceinline__ void seg_put4(int32_t w, const uint4& v, int lane)
+{
+    sDec.stg[w & 15][lane] = v.x;
+    sDec.stg[(w + 1) & 15][lane] = v.y;
+    sDec.stg[(w + 2) & 15][lane] = v.z;
+    sDec.stg[(w + 3) & 15][lane] = v.w;
+}
+// the first window of a reader at P: 4-word aligned, words P/32 - 15 .. P/32 at least
+__device__ __forceinline__ int32_t seg_first_wb(int32_t P) { return ((P >> 5) - 12) & ~3; }
+// the whole window [wb, wb + 16), loaded and staged at once (first round, walks, restarts)
+__device__ __forceinline__ void seg_stage_full(const SegRd& r, int32_t wb, int lane)
+{
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) v[i] = seg_load4(r, wb + 4 * i);
+#pragma unroll
+    for (int i = 0; i < 4; i++) seg_put4(wb + 4 * i, v[i], lane);
+}
 // reader at P from the staged window: W = words (P/32 - 1, P/32)
 __device__ __forceinline__ void seg_attach(SegRd& r, int32_t P, int lane)
 {
@@ -111,26 +132,21 @@ __device__ __forceinline__ uint32_t seg_entry1(SegRd& r, int lane, int32_t P, in
     return sDec.tab[(uint32_t)(r.W >> ((P - tl - r.wlo) & 63)) & tmask];
 }
 
-// 256-bit codeword-start bitmap: bit d = a start at (top - d)
+// 128-bit codeword-start bitmap: bit d = a start at (top - d)
 struct SegBm {
-    uint64_t q[4];
+    uint64_t q0, q1;
 };
 __device__ __forceinline__ bool bm_test(const SegBm& b, int32_t d)
 {
-    const uint64_t w = d < 64 ? b.q[0] : (d < 128 ? b.q[1] : (d < 192 ? b.q[2] : b.q[3]));
+    const uint64_t w = d < 64 ? b.q0 : b.q1;
     return d >= 0 && d < kSegRec && ((w >> (d & 63)) & 1ull) != 0;
 }
 // starts recorded above position top - d (bits below d)
 __device__ __forceinline__ uint32_t bm_below(const SegBm& b, int32_t d)
 {
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int32_t lo = 64 * i;
-        const uint64_t m = d >= lo + 64 ? ~0ull : (d <= lo ? 0ull : ((1ull << (d - lo)) - 1ull));
-        c += (uint32_t)__builtin_popcountll(b.q[i] & m);
-    }
-    return c;
+    const uint64_t m0 = d >= 64 ? ~0ull : (d <= 0 ? 0ull : ((1ull << d) - 1ull));
+    const uint64_t m1 = d >= 128 ? ~0ull : (d <= 64 ? 0ull : ((1ull << (d - 64)) - 1ull));
+    return (uint32_t)__builtin_popcountll(b.q0 & m0) + (uint32_t)__builtin_popcountll(b.q1 & m1);
 }
 
 // Returns false on a malformed section.  tl/minNb: the table in sDec.tab (tl <= kHufLdsLog) and its
@@ -206,15 +222,14 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
     bool main = active;            // decoding its segment
     bool done = !active;           // segment decoded and its exit synced
     uint32_t cnt = 0, skip = 0;
-    SegBm bm{{0, 0, 0, 0}};
+    SegBm bm{0, 0};
     // window room a single / a four / an eight-symbol step needs (the reader's refill word stays staged)
     const int32_t G1 = tli + 96, G4 = 4 * tli + 96, G8 = 8 * tli + 96;
-    uint4 pf[4];
-    if (main) {
-        rd.wb = seg_first_wb(Pp);
-        seg_fetch(rd, rd.wb, pf);
-    }
-    bool attach = main;  // the reader takes W/nx from the window once staged
+    uint4 pf[2];             // the next round's new half window: words [wb - 8, wb)
+    bool pe0 = false, pe1 = false;  // ... a piece of it across the stream's first byte
+    bool fresh = main;       // the window is staged whole before the first round (and after a restart)
+    bool attach = main;      // the reader takes W/nx from the window once staged
+    if (main) rd.wb = seg_first_wb(Pp);
     int epochs = 0;
     while (ballot(!done)) {
         if (++epochs > kSegMaxEpochs) return false;
@@ -222,14 +237,25 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
         while (ballot(main)) {
             P.count(1);
             if (main) {
-                seg_stage(rd.wb, pf, lane);
-                seg_fetch(rd, rd.wb - kSegStride, pf);
+                if (fresh) {
+                    seg_stage_full(rd, rd.wb, lane);
+                    fresh = false;
+                } else {  // move the window down by half: the prefetched words replace the consumed top
+                    rd.wb -= kSegStride;
+                    if (pe0) pf[0] = seg_load4(rd, rd.wb);
+                    if (pe1) pf[1] = seg_load4(rd, rd.wb + 4);
+                    seg_put4(rd.wb, pf[0], lane);
+                    seg_put4(rd.wb + 4, pf[1], lane);
+                }
+                pf[0] = seg_prefetch4(rd, rd.wb - 8, pe0);
+                pf[1] = seg_prefetch4(rd, rd.wb - 4, pe1);
             }
             lds_sync();
             if (attach) {
                 seg_attach(rd, Pp, lane);
                 attach = false;
             }
+            P.mark(11);
             const int32_t w32 = 32 * rd.wb;
             // singles: the overlap (no output), the recorded head, the alignment to four, the end
             while (true) {
@@ -244,10 +270,8 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
                     if (hd && spec && hi - Pp < kSegRec) {
                         const int32_t d = hi - Pp;
                         const uint64_t bit = 1ull << (d & 63);
-                        if (d < 64) bm.q[0] |= bit;
-                        else if (d < 128) bm.q[1] |= bit;
-                        else if (d < 192) bm.q[2] |= bit;
-                        else bm.q[3] |= bit;
+                        if (d < 64) bm.q0 |= bit;
+                        else bm.q1 |= bit;
                     }
                     if (hd) {
                         if (cnt < cap) gst<uint8_t>(reg + cnt, (uint8_t)e);
@@ -256,6 +280,7 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
                     Pp -= (int32_t)(e >> 8);
                 }
             }
+            P.mark(12);
             // bodies: eight symbols (two dword stores), then four, while the window and the segment
             // have room for that many codewords of the longest length
             const bool body = main && Pp <= hi && (cnt & 3u) == 0 && !(spec && hi - Pp < kSegRec);
@@ -295,6 +320,7 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
                     Pp = q;
                 }
             }
+            P.mark(13);
             // the last bits of the segment (reached in this round's bodies)
             while (true) {
                 const bool act = main && Pp <= hi && Pp > lo && Pp - w32 >= G1 && (Pp - lo < 4 * tli || cnt + 4u > cap);
@@ -307,21 +333,13 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
                     Pp -= (int32_t)(e >> 8);
                 }
             }
-            if (main) {
-                if (Pp <= lo) main = false;
-                else rd.wb -= kSegStride;
-            }
+            if (main && Pp <= lo) main = false;
+            P.mark(14);
         }
-        P.mark(12);
         // ---- sync of the lanes that finished their segment in this epoch: the exit against lane
         // j+1's start (its true start, or its recorded starts: DPP row_shl:1 within the row of 16)
-        uint64_t nb[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const uint32_t a = dpp<0x101>((uint32_t)bm.q[i]), b = dpp<0x101>((uint32_t)(bm.q[i] >> 32));
-            nb[i] = (uint64_t)a | ((uint64_t)b << 32);
-        }
-        const SegBm nbm{{nb[0], nb[1], nb[2], nb[3]}};
+        const SegBm nbm{(uint64_t)dpp<0x101>((uint32_t)bm.q0) | ((uint64_t)dpp<0x101>((uint32_t)(bm.q0 >> 32)) << 32),
+                        (uint64_t)dpp<0x101>((uint32_t)bm.q1) | ((uint64_t)dpp<0x101>((uint32_t)(bm.q1 >> 32)) << 32)};
         const bool nTrue = dpp<0x101>(tstart ? 1u : 0u) != 0u;
         const int32_t nPos = (int32_t)dpp<0x101>((uint32_t)spos);
         const bool syncing = !done;
@@ -333,8 +351,7 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
             P.count(5);
             if (walk) {
                 rd.wb = seg_first_wb(Pp);
-                seg_fetch(rd, rd.wb, pf);
-                seg_stage(rd.wb, pf, lane);
+                seg_stage_full(rd, rd.wb, lane);
             }
             lds_sync();
             if (walk) seg_attach(rd, Pp, lane);
@@ -362,7 +379,7 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
             }
         }
         if (ballot(bad)) return false;
-        P.mark(14);
+        P.mark(9);
         // deliveries to lane j+1 (DPP row_shr:1): the symbols it drops, or where to decode again from
         const bool endInWalk = synced && hasNext && !nTrue && Pp <= b8;  // lanes below hold nothing
         const uint32_t drop = (synced && hasNext && !nTrue && !endInWalk) ? bm_below(nbm, lo - Pp) : 0u;
@@ -381,7 +398,7 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
             done = false;
             if (main) {
                 rd.wb = seg_first_wb(Pp);
-                seg_fetch(rd, rd.wb, pf);
+                fresh = true;
                 attach = true;
             }
         }

@@ -10,7 +10,10 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <stdexcept>
 #include <vector>
 
@@ -83,21 +86,146 @@ thread_local char g_pod5_err[256];
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------------
+// Host copy workers: the pageable <-> pinned copies of the batch calls are split over a few
+// persistent threads (one thread moves ~5-10 GB/s; the batch calls need 20+ GB/s to keep up with
+// PCIe and the codec).  PGN_HOST_THREADS overrides the count (default min(8, hardware threads)).
+// ---------------------------------------------------------------------------------------------
+struct CopyJob {
+    uint8_t* dst;
+    const uint8_t* src;
+    size_t n;
+};
+
+class CopyPool {
+public:
+    explicit CopyPool(int nthreads)
+    {
+        for (int t = 1; t < nthreads; t++) th_.emplace_back([this, t] { worker(t); });
+        n_ = nthreads;
+    }
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    // all jobs, byte-balanced over the workers and the calling thread
+    void run(const CopyJob* jobs, size_t njobs)
+    {
+        size_t total = 0;
+        for (size_t i = 0; i < njobs; i++) total += jobs[i].n;
+        if (total == 0) return;
+        if (n_ == 1 || total < (1u << 20)) {
+            for (size_t i = 0; i < njobs; i++) memcpy(jobs[i].dst, jobs[i].src, jobs[i].n);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            jobs_ = jobs;
+            njobs_ = njobs;
+            total_ = total;
+            pending_ = n_ - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        share(0);
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+private:
+    // thread t copies bytes [t * total / n, (t + 1) * total / n) of the concatenated jobs
+    void share(int t)
+    {
+        const size_t a = total_ * (size_t)t / (size_t)n_, b = total_ * (size_t)(t + 1) / (size_t)n_;
+        size_t base = 0;
+        for (size_t i = 0; i < njobs_ && base < b; i++) {
+            const size_t lo = base, hi = base + jobs_[i].n;
+            base = hi;
+            if (hi <= a) continue;
+            const size_t x = lo < a ? a - lo : 0, y = (hi < b ? hi : b) - lo;
+            memcpy(jobs_[i].dst + x, jobs_[i].src + x, y - x);
+        }
+    }
+    void worker(int t)
+    {
+        uint64_t seen = 0;
+        while (true) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+            }
+            share(t);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    int n_ = 1;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const CopyJob* jobs_ = nullptr;
+    size_t njobs_ = 0, total_ = 0;
+    int pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+static int host_threads()
+{
+    if (const char* v = getenv("PGN_HOST_THREADS")) {
+        const int x = atoi(v);
+        if (x > 0) return x > 64 ? 64 : x;
+    }
+    const unsigned h = std::thread::hardware_concurrency();
+    return h == 0 ? 4 : (h < 8 ? (int)h : 8);
+}
+
+// sub-batch size of the pipelined calls (PGN_POD5_SUBBATCH_MB, default 32 MiB of input)
+static size_t sub_batch_bytes()
+{
+    if (const char* v = getenv("PGN_POD5_SUBBATCH_MB")) {
+        const long x = atol(v);
+        if (x > 0) return (size_t)x << 20;
+    }
+    return (size_t)32 << 20;
+}
+
+// A pinned host or device buffer that grows on demand (contents are not kept across growth).
+struct PinBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+};
+struct DevBuf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+};
+
 struct pgn_pod5_batch {
     pgn_ctx* ctx = nullptr;
     int codec = PGN_VARIANT_C5;
     uint32_t chunk = PGN_POD5_DEFAULT_CHUNK_SIZE;
-    hipStream_t stream = nullptr;
-    // pinned host staging, grown on demand
-    uint8_t* hBuf = nullptr;
-    size_t hBufCap = 0;
-    // device buffers, grown on demand
-    uint8_t* dBuf = nullptr;
-    size_t dBufCap = 0;
+    hipStream_t stream = nullptr;  // the context's stream: codec launches, scan and pack
+    hipStream_t copy = nullptr;    // host <-> device transfers
+    CopyPool* pool = nullptr;
+    // two pipeline slots: pinned staging and device buffers of one sub-batch each
+    PinBuf hIn[2], hMeta[2], hRes[2];
+    DevBuf dIn[2], dMeta[2], dOut[2], dPacked[2];
+    hipEvent_t evH2D[2] = {nullptr, nullptr}, evComp[2] = {nullptr, nullptr}, evD2H[2] = {nullptr, nullptr};
+    PinBuf hAll;  // compress: every packed blob of the call (what *out_data points to)
     // results of the last call (what the out pointers refer to)
     std::vector<uint64_t> offsets;
-    std::vector<uint8_t> data;
     std::vector<uint32_t> samples, readIndex;
+    std::vector<uint64_t> readStart;  // compress: first sample of each chunk within its read
 };
 
 #define P5CHK(x)                                                                                  \
@@ -111,28 +239,27 @@ struct pgn_pod5_batch {
 
 static size_t up256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-static int ensure_host(pgn_pod5_batch* b, size_t bytes)
+// grow a pinned / device buffer (the caller has made sure no queued work still uses it)
+static int ensure_pin(PinBuf& b, size_t bytes)
 {
-    if (bytes <= b->hBufCap) return PGN_OK;
-    if (b->hBuf) (void)hipHostFree(b->hBuf);
-    b->hBuf = nullptr;
+    if (bytes <= b.cap) return PGN_OK;
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
     const size_t cap = up256(bytes + bytes / 4);
-    P5CHK(hipHostMalloc((void**)&b->hBuf, cap, hipHostMallocDefault));
-    b->hBufCap = cap;
+    P5CHK(hipHostMalloc((void**)&b.p, cap, hipHostMallocDefault));
+    b.cap = cap;
     return PGN_OK;
 }
-
-static int ensure_dev(pgn_pod5_batch* b, size_t bytes)
+static int ensure_devbuf(DevBuf& b, size_t bytes)
 {
-    if (bytes <= b->dBufCap) return PGN_OK;
-    if (b->dBuf) {
-        (void)hipStreamSynchronize(b->stream);
-        (void)hipFree(b->dBuf);
-    }
-    b->dBuf = nullptr;
+    if (bytes <= b.cap) return PGN_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
     const size_t cap = up256(bytes + bytes / 4);
-    P5CHK(hipMalloc((void**)&b->dBuf, cap));
-    b->dBufCap = cap;
+    P5CHK(hipMalloc((void**)&b.p, cap));
+    b.cap = cap;
     return PGN_OK;
 }
 
@@ -166,6 +293,13 @@ static int batch_decompress(pgn_pod5_batch* b, size_t n, const uint8_t* d_in, co
                                                d_status, b->stream);
 }
 
+// every queued transfer and launch of the batch has finished
+static void batch_drain(pgn_pod5_batch* b)
+{
+    (void)hipStreamSynchronize(b->copy);
+    (void)hipStreamSynchronize(b->stream);
+}
+
 extern "C" {
 
 const char* pgn_pod5_last_error(void) { return g_pod5_err; }
@@ -181,6 +315,13 @@ int pgn_pod5_batch_create(pgn_ctx* ctx, int codec, uint32_t chunk_size, pgn_pod5
     b->codec = codec;
     b->chunk = chunk_size;
     b->stream = (hipStream_t)pgn_ctx_stream(ctx);
+    P5CHK(hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking));
+    for (int s = 0; s < 2; s++) {
+        P5CHK(hipEventCreateWithFlags(&b->evH2D[s], hipEventDisableTiming));
+        P5CHK(hipEventCreateWithFlags(&b->evComp[s], hipEventDisableTiming));
+        P5CHK(hipEventCreateWithFlags(&b->evD2H[s], hipEventDisableTiming));
+    }
+    b->pool = new CopyPool(host_threads());
     *out = b;
     return PGN_OK;
 }
@@ -188,13 +329,46 @@ int pgn_pod5_batch_create(pgn_ctx* ctx, int codec, uint32_t chunk_size, pgn_pod5
 int pgn_pod5_batch_destroy(pgn_pod5_batch* b)
 {
     if (!b) return PGN_ERR_INVALID_ARG;
-    (void)hipStreamSynchronize(b->stream);
-    if (b->dBuf) (void)hipFree(b->dBuf);
-    if (b->hBuf) (void)hipHostFree(b->hBuf);
+    batch_drain(b);
+    for (int s = 0; s < 2; s++) {
+        for (PinBuf* h : {&b->hIn[s], &b->hMeta[s], &b->hRes[s]})
+            if (h->p) (void)hipHostFree(h->p);
+        for (DevBuf* d : {&b->dIn[s], &b->dMeta[s], &b->dOut[s], &b->dPacked[s]})
+            if (d->p) (void)hipFree(d->p);
+        for (hipEvent_t e : {b->evH2D[s], b->evComp[s], b->evD2H[s]})
+            if (e) (void)hipEventDestroy(e);
+    }
+    if (b->hAll.p) (void)hipHostFree(b->hAll.p);
+    if (b->copy) (void)hipStreamDestroy(b->copy);
+    delete b->pool;
     delete b;
     return PGN_OK;
 }
 
+// Sub-batches of whole chunks (compress) or rows (decompress), about sub_batch_bytes() of input each.
+static void split_subs(const std::vector<uint64_t>& bytesPer, size_t n, std::vector<size_t>& bounds)
+{
+    const size_t target = sub_batch_bytes();
+    bounds.assign(1, 0);
+    size_t acc = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (acc > 0 && acc + bytesPer[i] > target) {
+            bounds.push_back(i);
+            acc = 0;
+        }
+        acc += bytesPer[i];
+    }
+    bounds.push_back(n);
+}
+
+// Compress pipeline over sub-batches j (chunks [c0, c1)), two slots s = j % 2:
+//   host   : the sub-batch's samples -> hIn[s] (copy workers), its per-chunk arrays -> hMeta[s];
+//   copy   : hIn/hMeta -> dIn/dMeta (after the compute of j - 2 has read them);
+//   stream : codec + scan + pack into dPacked[s] (after the download of j - 2 has read it), packed
+//            offsets and the first failing chunk -> hRes[s];
+//   then, one sub-batch behind: the host reads hRes and the copy stream downloads the packed blobs
+//   straight into the call's output (hAll), so that the packed bytes cross PCIe once and need no
+//   further host copy.
 int pgn_pod5_compress_reads(pgn_pod5_batch* b, uint32_t read_count, const int16_t* const* signal,
                             const uint32_t* signal_size, size_t* out_chunk_count, const uint64_t** out_offsets,
                             const uint8_t** out_data, const uint32_t** out_samples, const uint32_t** out_read_index)
@@ -205,158 +379,264 @@ int pgn_pod5_compress_reads(pgn_pod5_batch* b, uint32_t read_count, const int16_
     // the writer's chunking (file_writer.cpp:119-143): chunk k of a read = samples [k*cs, min((k+1)*cs, n))
     b->samples.clear();
     b->readIndex.clear();
-    size_t total = 0;
+    b->readStart.clear();
     for (uint32_t r = 0; r < read_count; r++) {
         if (signal_size[r] && !signal[r]) return PGN_ERR_INVALID_ARG;
         for (uint32_t s = 0; s < signal_size[r]; s += b->chunk) {
             b->samples.push_back(signal_size[r] - s < b->chunk ? signal_size[r] - s : b->chunk);
             b->readIndex.push_back(r);
+            b->readStart.push_back(s);
         }
-        total += signal_size[r];
     }
     const size_t n = b->samples.size();
     *out_chunk_count = 0;
     b->offsets.assign(n + 1, 0);
-    b->data.clear();
-    if (n == 0) {
-        *out_offsets = b->offsets.data();
-        *out_data = b->data.data();
-        *out_samples = b->samples.data();
-        *out_read_index = b->readIndex.data();
-        return PGN_OK;
-    }
-    // device layout: samples | sample offsets | counts | blob offsets | caps | sizes | status |
-    //                packed offsets (n + 1) | first bad | blobs (capacity-spaced) | packed blobs
-    uint64_t capTotal = 0;
-    for (size_t i = 0; i < n; i++) capTotal += chunk_cap(b->codec, b->samples[i]);
-    const size_t oSamples = 0, oSoff = up256(2 * total), oCnt = oSoff + up256(8 * n), oOoff = oCnt + up256(4 * n),
-                 oCaps = oOoff + up256(8 * n), oSizes = oCaps + up256(8 * n), oStatus = oSizes + up256(8 * n),
-                 oPoff = oStatus + up256(4 * n), oFirst = oPoff + up256(8 * (n + 1)), oBlobs = oFirst + 256,
-                 oPacked = oBlobs + up256(capTotal), devBytes = oPacked + up256(capTotal);
-    int rc = ensure_dev(b, devBytes);
-    if (rc) return rc;
-    // host staging: samples in, packed blobs out (the same region) | per-chunk arrays | offsets back
-    const size_t hostMeta = up256(8 * n) * 3 + up256(4 * n);
-    const size_t hBase = up256(2 * total > capTotal ? 2 * total : capTotal);
-    rc = ensure_host(b, hBase + hostMeta + up256(8 * (n + 1)) + 256);
-    if (rc) return rc;
-    // stage: the samples in read order (chunks of a read are contiguous), then the per-chunk arrays
-    uint8_t* h = b->hBuf;
-    size_t at = 0;
-    for (uint32_t r = 0; r < read_count; r++) {
-        if (signal_size[r]) memcpy(h + at, signal[r], 2 * (size_t)signal_size[r]);
-        at += 2 * (size_t)signal_size[r];
-    }
-    uint64_t* hSoff = (uint64_t*)(h + hBase);
-    uint32_t* hCnt = (uint32_t*)((uint8_t*)hSoff + up256(8 * n));
-    uint64_t* hOoff = (uint64_t*)((uint8_t*)hCnt + up256(4 * n));
-    uint64_t* hCaps = (uint64_t*)((uint8_t*)hOoff + up256(8 * n));
-    uint64_t so = 0, oo = 0;
-    for (size_t i = 0; i < n; i++) {
-        hSoff[i] = so;
-        hCnt[i] = b->samples[i];
-        hOoff[i] = oo;
-        hCaps[i] = chunk_cap(b->codec, b->samples[i]);
-        so += b->samples[i];
-        oo += hCaps[i];
-    }
-    uint8_t* d = b->dBuf;
-    P5CHK(hipMemcpyAsync(d + oSamples, h, 2 * total, hipMemcpyHostToDevice, b->stream));
-    P5CHK(hipMemcpyAsync(d + oSoff, hSoff, (uint8_t*)hCaps + 8 * n - (uint8_t*)hSoff, hipMemcpyHostToDevice, b->stream));
-    rc = batch_compress(b, n, (const int16_t*)(d + oSamples), (const uint64_t*)(d + oSoff), (const uint32_t*)(d + oCnt),
-                        d + oBlobs, (const uint64_t*)(d + oOoff), (const uint64_t*)(d + oCaps), (uint64_t*)(d + oSizes),
-                        (int32_t*)(d + oStatus));
-    if (rc) return rc;
-    hipLaunchKernelGGL(pod5_scan_kernel, dim3(1), dim3(1024), 0, b->stream, (const uint64_t*)(d + oSizes),
-                       (const int32_t*)(d + oStatus), (uint64_t*)(d + oPoff), (uint32_t*)(d + oFirst), (uint32_t)n);
-    hipLaunchKernelGGL(pod5_pack_kernel, dim3((unsigned)n), dim3(64), 0, b->stream, (const uint8_t*)(d + oBlobs),
-                       (const uint64_t*)(d + oOoff), (const uint64_t*)(d + oPoff), d + oPacked, (uint32_t)n);
-    P5CHK(hipGetLastError());
-    // offsets + first failing chunk back, then exactly the packed bytes
-    uint64_t* hPoff = (uint64_t*)(h + hBase + hostMeta);
-    uint32_t* hFirst = (uint32_t*)((uint8_t*)hPoff + up256(8 * (n + 1)));
-    P5CHK(hipMemcpyAsync(hPoff, d + oPoff, 8 * (n + 1), hipMemcpyDeviceToHost, b->stream));
-    P5CHK(hipMemcpyAsync(hFirst, d + oFirst, 4, hipMemcpyDeviceToHost, b->stream));
-    P5CHK(hipStreamSynchronize(b->stream));
-    if (*hFirst < n) {
-        int32_t s = 0;
-        P5CHK(hipMemcpy(&s, d + oStatus + 4 * (size_t)*hFirst, 4, hipMemcpyDeviceToHost));
-        *out_chunk_count = *hFirst;
-        return s ? s : PGN_ERR_INVALID_ARG;
-    }
-    memcpy(b->offsets.data(), hPoff, 8 * (n + 1));
-    const uint64_t packed = b->offsets[n];
-    P5CHK(hipMemcpyAsync(h, d + oPacked, packed, hipMemcpyDeviceToHost, b->stream));
-    P5CHK(hipStreamSynchronize(b->stream));
-    b->data.assign(h, h + packed);
-    *out_chunk_count = n;
     *out_offsets = b->offsets.data();
-    *out_data = b->data.data();
     *out_samples = b->samples.data();
     *out_read_index = b->readIndex.data();
+    *out_data = b->hAll.p;
+    if (n == 0) return PGN_OK;
+    std::vector<uint64_t> caps(n), inBytes(n);
+    uint64_t capAll = 0;
+    for (size_t i = 0; i < n; i++) {
+        caps[i] = chunk_cap(b->codec, b->samples[i]);
+        inBytes[i] = 2ull * b->samples[i];
+        capAll += caps[i];
+    }
+    std::vector<size_t> sb;
+    split_subs(inBytes, n, sb);
+    const size_t nsub = sb.size() - 1;
+    // slot sizes: the largest sub-batch
+    size_t maxIn = 0, maxCap = 0, maxN = 0;
+    for (size_t j = 0; j < nsub; j++) {
+        uint64_t a = 0, c = 0;
+        for (size_t i = sb[j]; i < sb[j + 1]; i++) {
+            a += inBytes[i];
+            c += caps[i];
+        }
+        maxIn = a > maxIn ? a : maxIn;
+        maxCap = c > maxCap ? c : maxCap;
+        maxN = sb[j + 1] - sb[j] > maxN ? sb[j + 1] - sb[j] : maxN;
+    }
+    // per-slot metadata: soff | cnt | ooff | caps (uploaded), sizes | status | poff | first (device)
+    const size_t mSoff = 0, mCnt = up256(8 * maxN), mOoff = mCnt + up256(4 * maxN), mCaps = mOoff + up256(8 * maxN),
+                 mUp = mCaps + up256(8 * maxN), mSizes = mUp, mStatus = mSizes + up256(8 * maxN),
+                 mPoff = mStatus + up256(4 * maxN), mFirst = mPoff + up256(8 * (maxN + 1)), mAll = mFirst + 256;
+    batch_drain(b);  // buffers may grow below
+    int rc = ensure_pin(b->hAll, capAll);
+    if (rc) return rc;
+    *out_data = b->hAll.p;
+    for (int s = 0; s < 2 && s < (int)nsub; s++) {
+        if ((rc = ensure_pin(b->hIn[s], maxIn)) || (rc = ensure_pin(b->hMeta[s], mUp)) ||
+            (rc = ensure_pin(b->hRes[s], up256(8 * (maxN + 1)) + 256)) || (rc = ensure_devbuf(b->dIn[s], maxIn)) ||
+            (rc = ensure_devbuf(b->dMeta[s], mAll)) || (rc = ensure_devbuf(b->dOut[s], maxCap)) ||
+            (rc = ensure_devbuf(b->dPacked[s], maxCap)))
+            return rc;
+    }
+    // read r's samples in this sub-batch: the chunks of a read are consecutive, so one copy per read run
+    std::vector<CopyJob> jobs;
+    uint64_t outBase = 0;
+    int err = PGN_OK;
+    size_t errChunk = n;
+    auto finish = [&](size_t j) -> int {  // results of sub-batch j
+        const int s = (int)(j & 1);
+        const size_t c0 = sb[j], m = sb[j + 1] - c0;
+        P5CHK(hipEventSynchronize(b->evComp[s]));
+        const uint64_t* poff = (const uint64_t*)b->hRes[s].p;
+        const uint32_t first = *(const uint32_t*)(b->hRes[s].p + up256(8 * (maxN + 1)));
+        if (first < m) {
+            int32_t st = 0;
+            P5CHK(hipMemcpy(&st, b->dMeta[s].p + mStatus + 4 * (size_t)first, 4, hipMemcpyDeviceToHost));
+            if (err == PGN_OK) {
+                err = st ? st : PGN_ERR_INVALID_ARG;
+                errChunk = c0 + first;
+            }
+            return PGN_OK;
+        }
+        if (err != PGN_OK) return PGN_OK;
+        for (size_t i = 0; i <= m; i++) b->offsets[c0 + i] = outBase + poff[i];
+        const uint64_t packed = poff[m];
+        P5CHK(hipStreamWaitEvent(b->copy, b->evComp[s], 0));
+        if (packed) P5CHK(hipMemcpyAsync(b->hAll.p + outBase, b->dPacked[s].p, packed, hipMemcpyDeviceToHost, b->copy));
+        P5CHK(hipEventRecord(b->evD2H[s], b->copy));
+        outBase += packed;
+        return PGN_OK;
+    };
+    for (size_t j = 0; j < nsub; j++) {
+        const int s = (int)(j & 1);
+        const size_t c0 = sb[j], m = sb[j + 1] - c0;
+        if (j >= 2) P5CHK(hipEventSynchronize(b->evH2D[s]));  // hIn/hMeta[s] free again
+        // samples of the sub-batch's chunks, one job per run of consecutive chunks of a read
+        jobs.clear();
+        uint64_t at = 0;
+        for (size_t i = c0; i < c0 + m;) {
+            const uint32_t r = b->readIndex[i];
+            size_t e = i;
+            uint64_t bytes = 0;
+            while (e < c0 + m && b->readIndex[e] == r) bytes += inBytes[e++];
+            jobs.push_back({b->hIn[s].p + at, (const uint8_t*)(signal[r] + b->readStart[i]), bytes});
+            at += bytes;
+            i = e;
+        }
+        b->pool->run(jobs.data(), jobs.size());
+        uint8_t* hm = b->hMeta[s].p;
+        uint64_t* hSoff = (uint64_t*)(hm + mSoff);
+        uint32_t* hCnt = (uint32_t*)(hm + mCnt);
+        uint64_t* hOoff = (uint64_t*)(hm + mOoff);
+        uint64_t* hCaps = (uint64_t*)(hm + mCaps);
+        uint64_t so = 0, oo = 0;
+        for (size_t i = 0; i < m; i++) {
+            hSoff[i] = so;
+            hCnt[i] = b->samples[c0 + i];
+            hOoff[i] = oo;
+            hCaps[i] = caps[c0 + i];
+            so += b->samples[c0 + i];
+            oo += caps[c0 + i];
+        }
+        if (j >= 2) P5CHK(hipStreamWaitEvent(b->copy, b->evComp[s], 0));  // compute j-2 has read dIn/dMeta[s]
+        P5CHK(hipMemcpyAsync(b->dIn[s].p, b->hIn[s].p, at, hipMemcpyHostToDevice, b->copy));
+        P5CHK(hipMemcpyAsync(b->dMeta[s].p, hm, mUp, hipMemcpyHostToDevice, b->copy));
+        P5CHK(hipEventRecord(b->evH2D[s], b->copy));
+        P5CHK(hipStreamWaitEvent(b->stream, b->evH2D[s], 0));
+        if (j >= 2) P5CHK(hipStreamWaitEvent(b->stream, b->evD2H[s], 0));  // download j-2 has read dPacked[s]
+        uint8_t* dm = b->dMeta[s].p;
+        rc = batch_compress(b, m, (const int16_t*)b->dIn[s].p, (const uint64_t*)(dm + mSoff),
+                            (const uint32_t*)(dm + mCnt), b->dOut[s].p, (const uint64_t*)(dm + mOoff),
+                            (const uint64_t*)(dm + mCaps), (uint64_t*)(dm + mSizes), (int32_t*)(dm + mStatus));
+        if (rc) {
+            batch_drain(b);
+            return rc;
+        }
+        hipLaunchKernelGGL(pod5_scan_kernel, dim3(1), dim3(1024), 0, b->stream, (const uint64_t*)(dm + mSizes),
+                           (const int32_t*)(dm + mStatus), (uint64_t*)(dm + mPoff), (uint32_t*)(dm + mFirst), (uint32_t)m);
+        hipLaunchKernelGGL(pod5_pack_kernel, dim3((unsigned)m), dim3(64), 0, b->stream, (const uint8_t*)b->dOut[s].p,
+                           (const uint64_t*)(dm + mOoff), (const uint64_t*)(dm + mPoff), b->dPacked[s].p, (uint32_t)m);
+        P5CHK(hipGetLastError());
+        P5CHK(hipMemcpyAsync(b->hRes[s].p, dm + mPoff, 8 * (m + 1), hipMemcpyDeviceToHost, b->stream));
+        P5CHK(hipMemcpyAsync(b->hRes[s].p + up256(8 * (maxN + 1)), dm + mFirst, 4, hipMemcpyDeviceToHost, b->stream));
+        P5CHK(hipEventRecord(b->evComp[s], b->stream));
+        if (j >= 1 && (rc = finish(j - 1))) {
+            batch_drain(b);
+            return rc;
+        }
+    }
+    rc = finish(nsub - 1);
+    batch_drain(b);
+    if (rc) return rc;
+    if (err != PGN_OK) {
+        *out_chunk_count = errChunk;
+        return err;
+    }
+    *out_chunk_count = n;
+    *out_data = b->hAll.p;
     return PGN_OK;
 }
 
+// Decompress pipeline over sub-batches of rows, two slots: the blobs -> hIn[s] (copy workers) ->
+// dIn[s]; decode into dOut[s]; samples and statuses -> hRes[s]; one sub-batch behind, the copy
+// workers move the samples to the caller's buffer while the next sub-batches are in flight.
 int pgn_pod5_decompress_rows(pgn_pod5_batch* b, uint32_t row_count, const uint64_t* offsets, const uint8_t* data,
                              const uint32_t* samples, int16_t* out, int32_t* row_status)
 {
     if (!b || (row_count && (!offsets || !samples))) return PGN_ERR_INVALID_ARG;
     if (row_count == 0) return PGN_OK;
     const size_t n = row_count;
-    const uint64_t bytes = offsets[n] - offsets[0];
-    if (offsets[n] < offsets[0] || (bytes && !data)) return PGN_ERR_INVALID_ARG;
+    if (offsets[n] < offsets[0] || (offsets[n] > offsets[0] && !data)) return PGN_ERR_INVALID_ARG;
     uint64_t total = 0;
+    std::vector<uint64_t> inBytes(n);
     for (size_t i = 0; i < n; i++) {
         if (offsets[i + 1] < offsets[i]) return PGN_ERR_INVALID_ARG;
+        inBytes[i] = offsets[i + 1] - offsets[i] + 2ull * samples[i] / 4;  // input plus a share of the output
         total += samples[i];
     }
     if (total && !out) return PGN_ERR_INVALID_ARG;
-    // device: blobs | blob offsets | blob sizes | sample offsets | counts | status | samples
-    const size_t oIn = 0, oIoff = up256(bytes), oIsz = oIoff + up256(8 * n), oSoff = oIsz + up256(8 * n),
-                 oCnt = oSoff + up256(8 * n), oStatus = oCnt + up256(4 * n), oOut = oStatus + up256(4 * n),
-                 devBytes = oOut + up256(2 * total);
-    int rc = ensure_dev(b, devBytes);
-    if (rc) return rc;
-    const size_t metaBytes = up256(8 * n) * 3 + up256(4 * n);
-    rc = ensure_host(b, (bytes > 2 * total ? bytes : 2 * total) + metaBytes + up256(4 * n));
-    if (rc) return rc;
-    uint8_t* h = b->hBuf;
-    if (bytes) memcpy(h, data + offsets[0], bytes);
-    uint64_t* hIoff = (uint64_t*)(h + up256(bytes > 2 * total ? bytes : 2 * total));
-    uint64_t* hIsz = (uint64_t*)((uint8_t*)hIoff + up256(8 * n));
-    uint64_t* hSoff = (uint64_t*)((uint8_t*)hIsz + up256(8 * n));
-    uint32_t* hCnt = (uint32_t*)((uint8_t*)hSoff + up256(8 * n));
-    int32_t* hStatus = (int32_t*)((uint8_t*)hCnt + up256(4 * n));
-    uint64_t so = 0;
-    for (size_t i = 0; i < n; i++) {
-        hIoff[i] = offsets[i] - offsets[0];
-        hIsz[i] = offsets[i + 1] - offsets[i];
-        hSoff[i] = so;
-        hCnt[i] = samples[i];
-        so += samples[i];
+    std::vector<size_t> sb;
+    split_subs(inBytes, n, sb);
+    const size_t nsub = sb.size() - 1;
+    size_t maxIn = 0, maxOut = 0, maxN = 0;
+    std::vector<uint64_t> sampleStart(n + 1, 0);
+    for (size_t i = 0; i < n; i++) sampleStart[i + 1] = sampleStart[i] + samples[i];
+    for (size_t j = 0; j < nsub; j++) {
+        const uint64_t a = offsets[sb[j + 1]] - offsets[sb[j]], o = 2 * (sampleStart[sb[j + 1]] - sampleStart[sb[j]]);
+        maxIn = a > maxIn ? a : maxIn;
+        maxOut = o > maxOut ? o : maxOut;
+        maxN = sb[j + 1] - sb[j] > maxN ? sb[j + 1] - sb[j] : maxN;
     }
-    uint8_t* d = b->dBuf;
-    if (bytes) P5CHK(hipMemcpyAsync(d + oIn, h, bytes, hipMemcpyHostToDevice, b->stream));
-    P5CHK(hipMemcpyAsync(d + oIoff, hIoff, (uint8_t*)hCnt + 4 * n - (uint8_t*)hIoff, hipMemcpyHostToDevice, b->stream));
-    rc = batch_decompress(b, n, d + oIn, (const uint64_t*)(d + oIoff), (const uint64_t*)(d + oIsz),
-                          (int16_t*)(d + oOut), (const uint64_t*)(d + oSoff), (const uint32_t*)(d + oCnt),
-                          (int32_t*)(d + oStatus));
-    if (rc) return rc;
-    P5CHK(hipMemcpyAsync(hStatus, d + oStatus, 4 * n, hipMemcpyDeviceToHost, b->stream));
-    if (total) P5CHK(hipMemcpyAsync(h, d + oOut, 2 * total, hipMemcpyDeviceToHost, b->stream));
-    P5CHK(hipStreamSynchronize(b->stream));
-    if (total) memcpy(out, h, 2 * total);
+    // metadata: ioff | isz | soff | cnt (uploaded), status (device, downloaded after the samples)
+    const size_t mIoff = 0, mIsz = up256(8 * maxN), mSoff = mIsz + up256(8 * maxN), mCnt = mSoff + up256(8 * maxN),
+                 mUp = mCnt + up256(4 * maxN), mStatus = mUp, mAll = mStatus + up256(4 * maxN);
+    batch_drain(b);
+    int rc;
+    for (int s = 0; s < 2 && s < (int)nsub; s++) {
+        if ((rc = ensure_pin(b->hIn[s], maxIn)) || (rc = ensure_pin(b->hMeta[s], mUp)) ||
+            (rc = ensure_pin(b->hRes[s], up256(maxOut) + up256(4 * maxN))) || (rc = ensure_devbuf(b->dIn[s], maxIn)) ||
+            (rc = ensure_devbuf(b->dMeta[s], mAll)) || (rc = ensure_devbuf(b->dOut[s], maxOut)))
+            return rc;
+    }
     int first = PGN_OK;
-    for (size_t i = 0; i < n; i++) {
-        if (row_status) row_status[i] = hStatus[i];
-        if (first == PGN_OK && hStatus[i] != PGN_OK) first = hStatus[i];
+    auto finish = [&](size_t j) -> int {  // samples and statuses of sub-batch j to the caller
+        const int s = (int)(j & 1);
+        const size_t r0 = sb[j], m = sb[j + 1] - r0;
+        P5CHK(hipEventSynchronize(b->evD2H[s]));
+        const uint64_t ob = 2 * (sampleStart[r0 + m] - sampleStart[r0]);
+        const CopyJob job{(uint8_t*)(out + sampleStart[r0]), b->hRes[s].p, ob};
+        b->pool->run(&job, 1);
+        const int32_t* st = (const int32_t*)(b->hRes[s].p + up256(maxOut));
+        for (size_t i = 0; i < m; i++) {
+            if (row_status) row_status[r0 + i] = st[i];
+            if (first == PGN_OK && st[i] != PGN_OK) first = st[i];
+        }
+        return PGN_OK;
+    };
+    for (size_t j = 0; j < nsub; j++) {
+        const int s = (int)(j & 1);
+        const size_t r0 = sb[j], m = sb[j + 1] - r0;
+        if (j >= 2) P5CHK(hipEventSynchronize(b->evH2D[s]));
+        const uint64_t bytes = offsets[r0 + m] - offsets[r0];
+        const CopyJob job{b->hIn[s].p, data + offsets[r0], bytes};
+        b->pool->run(&job, 1);
+        uint8_t* hm = b->hMeta[s].p;
+        uint64_t* hIoff = (uint64_t*)(hm + mIoff);
+        uint64_t* hIsz = (uint64_t*)(hm + mIsz);
+        uint64_t* hSoff = (uint64_t*)(hm + mSoff);
+        uint32_t* hCnt = (uint32_t*)(hm + mCnt);
+        for (size_t i = 0; i < m; i++) {
+            hIoff[i] = offsets[r0 + i] - offsets[r0];
+            hIsz[i] = offsets[r0 + i + 1] - offsets[r0 + i];
+            hSoff[i] = sampleStart[r0 + i] - sampleStart[r0];
+            hCnt[i] = samples[r0 + i];
+        }
+        if (j >= 2) P5CHK(hipStreamWaitEvent(b->copy, b->evComp[s], 0));
+        if (bytes) P5CHK(hipMemcpyAsync(b->dIn[s].p, b->hIn[s].p, bytes, hipMemcpyHostToDevice, b->copy));
+        P5CHK(hipMemcpyAsync(b->dMeta[s].p, hm, mUp, hipMemcpyHostToDevice, b->copy));
+        P5CHK(hipEventRecord(b->evH2D[s], b->copy));
+        P5CHK(hipStreamWaitEvent(b->stream, b->evH2D[s], 0));
+        if (j >= 2) P5CHK(hipStreamWaitEvent(b->stream, b->evD2H[s], 0));  // download j-2 has read dOut[s]
+        uint8_t* dm = b->dMeta[s].p;
+        rc = batch_decompress(b, m, b->dIn[s].p, (const uint64_t*)(dm + mIoff), (const uint64_t*)(dm + mIsz),
+                              (int16_t*)b->dOut[s].p, (const uint64_t*)(dm + mSoff), (const uint32_t*)(dm + mCnt),
+                              (int32_t*)(dm + mStatus));
+        if (rc) {
+            batch_drain(b);
+            return rc;
+        }
+        P5CHK(hipEventRecord(b->evComp[s], b->stream));
+        P5CHK(hipStreamWaitEvent(b->copy, b->evComp[s], 0));
+        const uint64_t ob = 2 * (sampleStart[r0 + m] - sampleStart[r0]);
+        if (ob) P5CHK(hipMemcpyAsync(b->hRes[s].p, b->dOut[s].p, ob, hipMemcpyDeviceToHost, b->copy));
+        P5CHK(hipMemcpyAsync(b->hRes[s].p + up256(maxOut), dm + mStatus, 4 * m, hipMemcpyDeviceToHost, b->copy));
+        P5CHK(hipEventRecord(b->evD2H[s], b->copy));
+        if (j >= 1 && (rc = finish(j - 1))) {
+            batch_drain(b);
+            return rc;
+        }
     }
+    rc = finish(nsub - 1);
+    batch_drain(b);
+    if (rc) return rc;
     return first;
 }
 
-// pgnano_pod5file.h: `copy --pgnano | --VBZ` of a file's signal table.  Device-resident between the
-// two launches: blobs up -> batched decode into one sample buffer -> batched encode -> device-side
-// pack -> packed blobs down.
 static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
                           int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats);
 

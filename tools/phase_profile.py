@@ -14,9 +14,9 @@ ENC = ["split", "search", "lit_gather", "hist", "sort", "hdr(writeCTable)", "huf
        "frame_finish", "assemble", "tree_merge", "tree_depth", "tree_maxheight", "tree_canon"]
 TWO = os.environ.get("PGN_HUF") != "seg"
 DEC = ["parse/merge_wait", "huf_table", "huf_copy(ph3)", "seq_list", "seq_exec", "raw_copy", "merge",
-       "lit_hdr", "huf_store(passB)", "-"] + (["-", "huf_spec(passA)", "huf_sync", "-", "-", "-"] if TWO else
-                                              ["seg_compact", "seg_head", "seg_body", "seg_tail", "seg_sync",
-                                               "seg_fallback"])
+       "lit_hdr", "huf_store(passB)"] + (["-", "-", "huf_spec(passA)", "huf_sync", "-", "-", "-"] if TWO else
+                                         ["seg_sync+walk", "seg_compact", "seg_stage", "seg_singles", "seg_bodies",
+                                          "seg_tail", "seg_epochs"])
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 S = 100000
 c = PGNanoCodec(0)
@@ -40,9 +40,9 @@ for name, lab, arr in (("encode", ENC, buf[:16]), ("decode", DEC, buf[16:])):
 
 DCNT = (["huf rounds", "passA overlap iters", "passA bitmap iters", "passA main4 iters", "passA tail iters",
          "sync iters", "sync iters with walks"] if TWO else
-        ["huf sections", "seg overlap iters", "seg head iters", "seg body groups(16)", "seg tail iters",
-         "seg walk iters", "seg fallback sections"]) + [
-        "passB 4-sym iters", "passB 1-sym iters", "huf tables", "-", "seq blocks", "blocks", "frames", "raw bytes", "-"]
+        ["huf sections", "seg rounds", "seg single iters", "seg body8 iters", "seg tail iters",
+         "seg walk rounds", "-", "seg body4 iters"]) + [
+        "passB 1-sym iters", "huf tables", "-", "seq blocks", "blocks", "frames", "raw bytes", "-"]
 print("decode counters per chunk:")
 for i, l in enumerate(DCNT):
     if buf[48 + i]:
