@@ -154,8 +154,9 @@ __device__ __forceinline__ uint32_t bm_below(const SegBm& b, int32_t d)
 // segBuf/segCap: scratch for the segment regions (16-byte aligned).
 __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, const uint8_t* hp, size_t remain,
                                                   uint8_t* dst, uint32_t rs, uint32_t jt01, uint32_t jt2,
-                                                  uint8_t* segBuf, size_t segCap, PhaseProf& P)
+                                                  uint8_t* segBuf, size_t segCap, PhaseProf& P, uint32_t diag = 0)
 {
+    diag = uni(diag);
     const int lane = lane_id();
     tl = uni(tl);
     minNb = uni(minNb);
@@ -299,7 +300,7 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
                     }
                     const uint32_t w0 = (e[0] & 0xFFu) | ((e[1] & 0xFFu) << 8) | ((e[2] & 0xFFu) << 16) | (e[3] << 24);
                     const uint32_t w1 = (e[4] & 0xFFu) | ((e[5] & 0xFFu) << 8) | ((e[6] & 0xFFu) << 16) | (e[7] << 24);
-                    gst<uint64_t>(reg + cnt, (uint64_t)w0 | ((uint64_t)w1 << 32));
+                    if (!(diag & 1u)) gst<uint64_t>(reg + cnt, (uint64_t)w0 | ((uint64_t)w1 << 32));
                     cnt += 8;
                     Pp = q;
                 }
@@ -415,8 +416,8 @@ __device__ __noinline__ bool huf_seg_decode4_wave(unsigned tl, unsigned minNb, c
     incl += dpp<0x114>(incl);
     incl += dpp<0x118>(incl);
     const uint32_t tot = (uint32_t)__shfl((int)incl, lane | 15, 64);
-    if (ballot(bad || tot != nsym)) return false;
-    if (S == 1) return true;
+    if (ballot(bad || tot != nsym) && !(diag & 4u)) return false;
+    if (S == 1 || (diag & 2u)) return true;
     // ---- compaction: every lane copies its valid bytes to the stream's place in the destination
     if (v > 0) {
         const uint8_t* a = reg + skip;

@@ -282,6 +282,7 @@ struct DecArgs {
     size_t base, G;
     uint32_t nu;         // zstd work units per chunk: 5 (C5) or 1 (VBZ)
     uint32_t segCap;     // Huffman segment scratch per slot; 0 = the two-pass decoder (PGN_HUF=twopass)
+    uint32_t segDiag;    // PGN_SEG_DIAG (timing experiments)
 };
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
@@ -338,6 +339,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     S.htab = (uint16_t*)(sbase + lay.htab);
     S.seg = sbase + lay.seg;
     S.segCap = a.segCap;
+    S.segDiag = a.segDiag;
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = (size_t)a.nu * G;
@@ -361,7 +363,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     P.flush();
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(7))) void dec_merge_kernel(DecArgs a)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void dec_merge_kernel(DecArgs a)
 {
     const size_t g = blockIdx.x;
     const size_t c = a.base + g;
@@ -801,6 +803,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.htab = (uint16_t*)(sbase + lay.htab);
     S.seg = sbase + lay.seg;
     S.segCap = a.segCap;
+    S.segDiag = a.segDiag;
     uint8_t* inter = sbase + lay.bytes;
     PhaseProf P;
     P.init(a.prof);
@@ -962,6 +965,7 @@ struct pgn_ctx {
     size_t encFusedSlotsMax = 0, decFusedSlotsMax = 0;
     size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH, staged pipeline)
     uint32_t hufSegCap = 0;  // the one-pass Huffman decoder (PGN_HUF=seg) or the two-pass one (0, default)
+    uint32_t segDiag = 0;    // PGN_SEG_DIAG: timing experiments on the one-pass decoder (wrong output)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
@@ -1077,6 +1081,7 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         c->encForced = true;
     }
     if (const char* pp = getenv("PGN_DEC_PIPELINE")) c->decStaged = strcmp(pp, "staged") == 0;
+    if (const char* dg = getenv("PGN_SEG_DIAG")) c->segDiag = (uint32_t)atoi(dg);
     if (const char* h = getenv("PGN_HUF")) c->hufSegCap = strcmp(h, "seg") == 0 ? (uint32_t)kSegScratch : 0u;
     if (const char* sb = getenv("PGN_SUBBATCH")) {
         long v = atol(sb);
@@ -1274,6 +1279,7 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.queue = c->queues;
     a.segCap = c->hufSegCap;
+    a.segDiag = c->segDiag;
     c->lastUnits = nullptr;
     switch (codec) {
     case kCodecC5: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
@@ -1397,6 +1403,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.G = G;
     a.nu = nu;
     a.segCap = c->hufSegCap;
+    a.segDiag = c->segDiag;
     // pass p: parse + zstd on the caller's stream into buffer p % 2, merge on the side stream.  The
     // merge of pass p overlaps the zstd kernel of pass p+1; a buffer is parsed into again only after
     // the merge of the pass before last has read it.

@@ -74,6 +74,7 @@ struct DecScratch {
     uint16_t* htab;         // 4096 entries: a 12-bit Huffman table, or the parked LDS table
     uint8_t* seg;           // segment regions of the one-pass Huffman decoder (pgn_hufseg.h)
     uint32_t segCap;        // their bytes; 0 selects the two-pass decoder (pgn_huf4.h)
+    uint32_t segDiag;       // diagnostic switches (PGN_SEG_DIAG, timing experiments only; wrong output)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -874,6 +875,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     S.htab = uni(S.htab);
     S.seg = uni(S.seg);
     S.segCap = uni(S.segCap);
+    S.segDiag = uni(S.segDiag);
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
     HdrWin hw;
@@ -1016,7 +1018,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                             const uint32_t jt2 = hw_u16(hw, src, jp + 4);
                             if (S.segCap)
                                 ok = huf_seg_decode4_wave(hufTl, hufMinNb, hp, remain, litOut, (uint32_t)rs, jt01, jt2,
-                                                          S.seg, S.segCap, P);
+                                                          S.seg, S.segCap, P, S.segDiag);
                             else
                                 ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, P);
                         }

@@ -126,7 +126,10 @@ def test_bench_rank_body_weak_scaling_two_ranks():
 
 
 def test_bench_rank_body_strong_scaling_batches():
-    """--global-reads: a fixed read set split round-robin over the ranks, in resident batches."""
+    """--global-reads: a fixed read set split round-robin over the ranks, in batches of DISTINCT reads:
+    the reported compressed bytes are those of every one of the G reads (measured, not extrapolated)."""
+    import _oracle as O
+
     reads_total, n = 7, 1500
     res = _run_bench_ranks(2, ["--global-reads", str(reads_total), "--reads", "2", "--samples", str(n),
                                "--steps", "1", "--warmup", "0", "--no-side", "--no-cpu-baseline"])
@@ -134,6 +137,12 @@ def test_bench_rank_body_strong_scaling_batches():
     assert line["scaling"] == "strong" and line["round_trip_ok"]
     assert line["config"]["global_reads"] == reads_total
     assert line["config"]["reads_per_gpu"] == 4  # rank 0 owns reads 0, 2, 4, 6
+    want = sum(len(O.c5_compress(O.synth_read(g, n))[1]) for g in range(reads_total))
+    assert line["compressed_bytes"] == want
+    # the same read set held resident (one batch per rank): same bytes
+    res1 = _run_bench_ranks(2, ["--global-reads", str(reads_total), "--samples", str(n), "--steps", "1",
+                                "--warmup", "0", "--no-side", "--no-cpu-baseline"])
+    assert res1[0]["compressed_bytes"] == want and "resident" in res1[0]["config"]["workload"]
 
 
 def test_rank_batches_partition():
@@ -150,6 +159,10 @@ def test_rank_batches_partition():
         assert tot == G
     mine, batches, scaling = bench.rank_batches(bench.parse([]), 0, 4)
     assert (mine, batches, scaling) == (100_000, [100_000], "weak")
+    # configs[3] at 8 GPUs: a rank's 125,000 reads (75 GB at 6 B/sample) stay resident in one batch
+    assert bench.rank_batches(bench.parse(["--global-reads", "1000000"]), 3, 8) == (125_000, [125_000], "strong")
+    mine, batches, _ = bench.rank_batches(bench.parse(["--global-reads", "1000000"]), 0, 1)
+    assert mine == 1_000_000 and len(batches) == 4 and max(batches) <= 333_333
 
 
 def test_launcher_gives_each_rank_torchrun_env(tmp_path):
