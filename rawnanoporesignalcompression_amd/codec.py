@@ -386,7 +386,9 @@ class Pod5SignalBatch:
         except Exception:
             pass
 
-    def compress_reads(self, reads):
+    def compress_reads(self, reads, copy: bool = True):
+        """(offsets, data, samples, read_index) of the chunked, compressed reads.  copy=False returns
+        views of the batch's own buffers, valid until its next call (as in the C API)."""
         xs = [np.ascontiguousarray(r, dtype=np.int16) for r in reads]
         ptrs = (C.c_void_p * max(len(xs), 1))(*[x.ctypes.data if x.size else None for x in xs])
         sizes = np.array([x.size for x in xs] or [0], dtype=np.uint32)
@@ -396,14 +398,15 @@ class Pod5SignalBatch:
                                                C.byref(pd), C.byref(ps), C.byref(pr))
         _check(rc, f"chunk {n.value}" if rc else "")
         k = n.value
-        offsets = np.ctypeslib.as_array((C.c_uint64 * (k + 1)).from_address(po.value)).copy()
-        data = (np.ctypeslib.as_array((C.c_uint8 * int(offsets[-1])).from_address(pd.value)).copy()
+        cp = (lambda a: a.copy()) if copy else (lambda a: a)
+        offsets = cp(np.ctypeslib.as_array((C.c_uint64 * (k + 1)).from_address(po.value)))
+        data = (cp(np.ctypeslib.as_array((C.c_uint8 * int(offsets[-1])).from_address(pd.value)))
                 if offsets[-1] else np.zeros(0, np.uint8))
-        samples = np.ctypeslib.as_array((C.c_uint32 * k).from_address(ps.value)).copy() if k else np.zeros(0, np.uint32)
-        read_index = np.ctypeslib.as_array((C.c_uint32 * k).from_address(pr.value)).copy() if k else np.zeros(0, np.uint32)
+        samples = cp(np.ctypeslib.as_array((C.c_uint32 * k).from_address(ps.value))) if k else np.zeros(0, np.uint32)
+        read_index = cp(np.ctypeslib.as_array((C.c_uint32 * k).from_address(pr.value))) if k else np.zeros(0, np.uint32)
         return offsets, data, samples, read_index
 
-    def decompress_rows(self, offsets, data, samples):
+    def decompress_rows(self, offsets, data, samples, out=None):
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         data = np.ascontiguousarray(data, dtype=np.uint8)
         samples = np.ascontiguousarray(samples, dtype=np.uint32)
@@ -413,8 +416,12 @@ class Pod5SignalBatch:
             raise ValueError(f"offsets has {offsets.size} entries, expected rows + 1 = {k + 1}")
         if k and (int(offsets[-1]) > data.size or np.any(np.diff(offsets.astype(np.int64)) < 0)):
             raise ValueError("offsets are not monotonic or run past the data buffer")
-        out = np.empty(max(int(samples.sum()), 1), dtype=np.int16)
+        total = int(samples.sum())
+        if out is None:
+            out = np.empty(max(total, 1), dtype=np.int16)
+        elif out.dtype != np.int16 or not out.flags.c_contiguous or out.size < total:
+            raise ValueError("out must be a contiguous int16 array of at least sum(samples) entries")
         st = np.zeros(max(k, 1), dtype=np.int32)
         _check(self._lib.pgn_pod5_decompress_rows(self._h, k, offsets.ctypes.data, data.ctypes.data if data.size else None,
                                                   samples.ctypes.data, out.ctypes.data, st.ctypes.data))
-        return out[: int(samples.sum())]
+        return out[:total]
