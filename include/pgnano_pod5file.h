@@ -84,6 +84,16 @@ int pgn_pod5_signal_info(const pgn_pod5_file *f, uint64_t *rows, uint32_t *batch
 int pgn_pod5_signal_read(const pgn_pod5_file *f, uint8_t *read_ids, uint32_t *samples, uint64_t *offsets,
                          uint8_t *data);
 
+/* The rows of signal record batch `batch`: rows first_row .. first_row + rows - 1 of the table. */
+int pgn_pod5_signal_batch_rows(const pgn_pod5_file *f, uint32_t batch, uint64_t *first_row, uint64_t *rows);
+
+/* The rows of the record batches batch_ids[0 .. n), in that order, copied out as
+ * pgn_pod5_signal_read does (offsets relative to this selection; any array may be NULL).  With the
+ * arrays NULL it reports the selection's rows, data bytes and samples, to size them. */
+int pgn_pod5_signal_read_batches(const pgn_pod5_file *f, const uint32_t *batch_ids, uint32_t n, uint64_t *rows,
+                                 uint64_t *data_bytes, uint64_t *total_samples, uint8_t *read_ids, uint32_t *samples,
+                                 uint64_t *offsets, uint8_t *data);
+
 /* Writes a combined POD5 file whose signal table holds the given rows (row i: read_ids[16 i ..],
  * samples[i], signal bytes data[offsets[i] .. offsets[i + 1])) as `signal_type`, in record batches
  * of rows_per_batch rows (0 = 100).
@@ -115,6 +125,20 @@ typedef struct pgn_pod5_transcode_stats {
  * pgn_pod5_last_error, pgnano_pod5.h). */
 int pgn_pod5_transcode_file(pgn_ctx *ctx, const char *in_path, const char *out_path, int dst_signal_type,
                             int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats *stats);
+
+/* One rank's share of a multi-GPU `copy` (the reference's writer takes whole read batches,
+ * c_api.cpp:1104-1110; its reader decodes record batches, signal_table_reader.cpp:294-318): the
+ * signal column of record batches batch_ids[0 .. n) of `f`, in that order, transcoded on ctx's GPU
+ * exactly as pgn_pod5_transcode_file does.  The ranks' parts, put back in record-batch order, are
+ * the column pgn_pod5_transcode_file writes (the caller gathers them and writes the file with
+ * pgn_pod5_write_file).  The result is owned by *out: pgn_pod5_part_get, then pgn_pod5_part_free. */
+typedef struct pgn_pod5_part pgn_pod5_part;
+int pgn_pod5_transcode_part(pgn_ctx *ctx, const pgn_pod5_file *f, const uint32_t *batch_ids, uint32_t n,
+                            int dst_signal_type, int pgnano_variant, pgn_pod5_part **out,
+                            pgn_pod5_transcode_stats *stats);
+/* rows of the part; offsets: rows + 1 entries into data (offsets[0] = 0). Valid until part_free. */
+int pgn_pod5_part_get(const pgn_pod5_part *part, uint64_t *rows, const uint64_t **offsets, const uint8_t **data);
+int pgn_pod5_part_free(pgn_pod5_part *part);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -659,30 +660,18 @@ int pgn_pod5_transcode_file(pgn_ctx* ctx, const char* in_path, const char* out_p
 
 }  // extern "C"
 
-static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
-                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats)
+// One device pass over a signal column: decode (unless uncompressed), re-encode as dst_signal_type,
+// pack on the device, download the packed column.  outOffs gets n + 1 offsets into outData.
+static int transcode_rows(pgn_ctx* ctx, int srcType, int dst_signal_type, int pgnano_variant, size_t n,
+                          const std::vector<uint32_t>& samples, const std::vector<uint64_t>& offs,
+                          const std::vector<uint8_t>& data, uint64_t dataBytes, uint64_t total,
+                          std::vector<uint64_t>& outOffs, std::vector<uint8_t>& outData, float& decMs, float& encMs)
 {
-    if (!ctx || !in_path || !out_path || dst_signal_type < PGN_POD5_SIGNAL_UNCOMPRESSED ||
-        dst_signal_type > PGN_POD5_SIGNAL_PGNANO || pgnano_variant < PGN_VARIANT_C5 || pgnano_variant > PGN_VARIANT_VBZ0)
-        return PGN_ERR_INVALID_ARG;
-    pgn_pod5_file* f = nullptr;
-    int rc = pgn_pod5_file_open(in_path, &f);
-    if (rc) {
-        snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", pgn_pod5_file_error());
-        return rc;
-    }
-    uint64_t rows = 0, dataBytes = 0, total = 0;
-    uint32_t nb = 0;
-    int srcType = 0;
-    pgn_pod5_signal_info(f, &rows, &nb, &srcType, &dataBytes, &total);
-    std::vector<uint8_t> ids(16 * rows), data(dataBytes), outData;
-    std::vector<uint32_t> samples(rows);
-    std::vector<uint64_t> offs(rows + 1), outOffs(rows + 1, 0);
-    pgn_pod5_signal_read(f, ids.data(), samples.data(), offs.data(), data.data());
+    outOffs.assign(n + 1, 0);
+    outData.clear();
+    decMs = encMs = 0;
     const int srcCodec = srcType == PGN_POD5_SIGNAL_VBZ ? PGN_POD5_CODEC_VBZ : pgnano_variant;
     const int dstCodec = dst_signal_type == PGN_POD5_SIGNAL_VBZ ? PGN_POD5_CODEC_VBZ : pgnano_variant;
-    const size_t n = (size_t)rows;
-    float decMs = 0, encMs = 0;
     uint8_t* d = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     const hipStream_t stream = (hipStream_t)pgn_ctx_stream(ctx);
@@ -788,15 +777,44 @@ static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_pat
         P5CHK(hipStreamSynchronize(stream));
         return PGN_OK;
     };
-    rc = body();
+    int rc = body();
     if (d) {
         (void)hipStreamSynchronize(stream);
         (void)hipFree(d);
     }
     for (auto& e : ev)
         if (e) (void)hipEventDestroy(e);
-    if (rc == PGN_OK)
-    {
+    return rc;
+}
+
+static bool transcode_args_ok(pgn_ctx* ctx, int dst_signal_type, int pgnano_variant)
+{
+    return ctx && dst_signal_type >= PGN_POD5_SIGNAL_UNCOMPRESSED && dst_signal_type <= PGN_POD5_SIGNAL_PGNANO &&
+           pgnano_variant >= PGN_VARIANT_C5 && pgnano_variant <= PGN_VARIANT_VBZ0;
+}
+
+static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
+                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats)
+{
+    if (!in_path || !out_path || !transcode_args_ok(ctx, dst_signal_type, pgnano_variant)) return PGN_ERR_INVALID_ARG;
+    pgn_pod5_file* f = nullptr;
+    int rc = pgn_pod5_file_open(in_path, &f);
+    if (rc) {
+        snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", pgn_pod5_file_error());
+        return rc;
+    }
+    uint64_t rows = 0, dataBytes = 0, total = 0;
+    uint32_t nb = 0;
+    int srcType = 0;
+    pgn_pod5_signal_info(f, &rows, &nb, &srcType, &dataBytes, &total);
+    std::vector<uint8_t> ids(16 * rows), data(dataBytes), outData;
+    std::vector<uint32_t> samples(rows);
+    std::vector<uint64_t> offs(rows + 1), outOffs;
+    pgn_pod5_signal_read(f, ids.data(), samples.data(), offs.data(), data.data());
+    float decMs = 0, encMs = 0;
+    rc = transcode_rows(ctx, srcType, dst_signal_type, pgnano_variant, (size_t)rows, samples, offs, data, dataBytes,
+                        total, outOffs, outData, decMs, encMs);
+    if (rc == PGN_OK) {
         rc = pgn_pod5_write_file(out_path, f, dst_signal_type, rows, ids.data(), samples.data(), outOffs.data(),
                                  outData.data(), rows_per_batch, nullptr, nullptr);
         if (rc) snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", pgn_pod5_file_error());
@@ -805,12 +823,90 @@ static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_pat
         stats->rows = rows;
         stats->samples = total;
         stats->in_bytes = dataBytes;
-        stats->out_bytes = outOffs[n];
+        stats->out_bytes = outOffs[rows];
         stats->decode_ms = decMs;
         stats->encode_ms = encMs;
     }
     pgn_pod5_file_close(f);
     return rc;
 }
+
+struct pgn_pod5_part {
+    std::vector<uint64_t> offsets;
+    std::vector<uint8_t> data;
+};
+
+static int transcode_part_impl(pgn_ctx* ctx, const pgn_pod5_file* f, const uint32_t* batch_ids, uint32_t nIds,
+                               int dst_signal_type, int pgnano_variant, pgn_pod5_part** out,
+                               pgn_pod5_transcode_stats* stats)
+{
+    if (!f || !out || (nIds && !batch_ids) || !transcode_args_ok(ctx, dst_signal_type, pgnano_variant))
+        return PGN_ERR_INVALID_ARG;
+    *out = nullptr;
+    uint64_t rows = 0, dataBytes = 0, total = 0, allRows = 0;
+    uint32_t nb = 0;
+    int srcType = 0;
+    pgn_pod5_signal_info(f, &allRows, &nb, &srcType, nullptr, nullptr);
+    int rc = pgn_pod5_signal_read_batches(f, batch_ids, nIds, &rows, &dataBytes, &total, nullptr, nullptr, nullptr,
+                                          nullptr);
+    if (rc) {
+        snprintf(g_pod5_err, sizeof(g_pod5_err), "batch id out of range (%u record batches)", nb);
+        return rc;
+    }
+    std::vector<uint8_t> data(dataBytes);
+    std::vector<uint32_t> samples(rows);
+    std::vector<uint64_t> offs(rows + 1);
+    pgn_pod5_signal_read_batches(f, batch_ids, nIds, nullptr, nullptr, nullptr, nullptr, samples.data(), offs.data(),
+                                 data.data());
+    std::unique_ptr<pgn_pod5_part> part(new pgn_pod5_part);
+    float decMs = 0, encMs = 0;
+    rc = transcode_rows(ctx, srcType, dst_signal_type, pgnano_variant, (size_t)rows, samples, offs, data, dataBytes,
+                        total, part->offsets, part->data, decMs, encMs);
+    if (rc) return rc;
+    if (stats) {
+        stats->rows = rows;
+        stats->samples = total;
+        stats->in_bytes = dataBytes;
+        stats->out_bytes = part->offsets[rows];
+        stats->decode_ms = decMs;
+        stats->encode_ms = encMs;
+    }
+    *out = part.release();
+    return PGN_OK;
+}
+
+extern "C" {
+
+int pgn_pod5_transcode_part(pgn_ctx* ctx, const pgn_pod5_file* f, const uint32_t* batch_ids, uint32_t n,
+                            int dst_signal_type, int pgnano_variant, pgn_pod5_part** out,
+                            pgn_pod5_transcode_stats* stats)
+{
+    try {
+        return transcode_part_impl(ctx, f, batch_ids, n, dst_signal_type, pgnano_variant, out, stats);
+    } catch (const std::bad_alloc&) {
+        snprintf(g_pod5_err, sizeof(g_pod5_err), "out of host memory");
+        return PGN_ERR_IO;
+    } catch (const std::exception& e) {
+        snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", e.what());
+        return PGN_ERR_CORRUPT;
+    }
+}
+
+int pgn_pod5_part_get(const pgn_pod5_part* part, uint64_t* rows, const uint64_t** offsets, const uint8_t** data)
+{
+    if (!part) return PGN_ERR_INVALID_ARG;
+    if (rows) *rows = part->offsets.size() - 1;
+    if (offsets) *offsets = part->offsets.data();
+    if (data) *data = part->data.data();
+    return PGN_OK;
+}
+
+int pgn_pod5_part_free(pgn_pod5_part* part)
+{
+    delete part;
+    return PGN_OK;
+}
+
+}  // extern "C"
 
 

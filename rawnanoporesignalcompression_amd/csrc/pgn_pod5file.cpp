@@ -900,6 +900,50 @@ int pgn_pod5_signal_read(const pgn_pod5_file* f, uint8_t* read_ids, uint32_t* sa
     return PGN_OK;
 }
 
+int pgn_pod5_signal_batch_rows(const pgn_pod5_file* f, uint32_t batch, uint64_t* first_row, uint64_t* rows)
+{
+    if (!f || batch >= f->batches.size()) return PGN_ERR_INVALID_ARG;
+    uint64_t r0 = 0;
+    for (uint32_t b = 0; b < batch; b++) r0 += f->batches[b].rows;
+    if (first_row) *first_row = r0;
+    if (rows) *rows = f->batches[batch].rows;
+    return PGN_OK;
+}
+
+int pgn_pod5_signal_read_batches(const pgn_pod5_file* f, const uint32_t* batch_ids, uint32_t n, uint64_t* rows_out,
+                                 uint64_t* data_bytes_out, uint64_t* samples_out, uint8_t* read_ids, uint32_t* samples,
+                                 uint64_t* offsets, uint8_t* data)
+{
+    if (!f || (n && !batch_ids)) return PGN_ERR_INVALID_ARG;
+    const uint64_t scale = f->signal_type == PGN_POD5_SIGNAL_UNCOMPRESSED ? 2 : 1;
+    uint64_t row = 0, at = 0, tot = 0;
+    if (offsets) offsets[0] = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (batch_ids[i] >= f->batches.size()) return PGN_ERR_INVALID_ARG;
+        const SignalBatch& b = f->batches[batch_ids[i]];
+        if (read_ids) memcpy(read_ids + 16 * row, b.read_ids, 16 * b.rows);
+        if (samples) memcpy(samples + row, b.samples, 4 * b.rows);
+        for (uint64_t r = 0; r < b.rows; r++) {
+            uint32_t sm;
+            memcpy(&sm, (const uint8_t*)b.samples + 4 * r, 4);
+            tot += sm;
+        }
+        const uint64_t first = (uint64_t)ld_i64(b.offsets) * scale;
+        for (uint64_t r = 0; r < b.rows; r++) {
+            const uint64_t end = (uint64_t)ld_i64(b.offsets + 8 * (r + 1)) * scale;
+            if (offsets) offsets[row + r + 1] = at + end - first;
+        }
+        const uint64_t m = (uint64_t)ld_i64(b.offsets + 8 * b.rows) * scale - first;
+        if (data && m) memcpy(data + at, b.data + first, m);
+        at += m;
+        row += b.rows;
+    }
+    if (rows_out) *rows_out = row;
+    if (data_bytes_out) *data_bytes_out = at;
+    if (samples_out) *samples_out = tot;
+    return PGN_OK;
+}
+
 int pgn_pod5_write_file(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,
                         const uint8_t* read_ids, const uint32_t* samples, const uint64_t* offsets, const uint8_t* data,
                         uint32_t rows_per_batch, const char* software, const uint8_t* section_marker)

@@ -9,7 +9,10 @@ with the signal column decoded and re-encoded by batched GPU launches.
 * :class:`Pod5File` -- footer strings, embedded files, and the signal table as numpy arrays
   (read ids, samples, byte offsets, signal bytes);
 * :func:`write_pod5` -- a combined file from signal-table rows, copying the other tables of a source;
-* :func:`transcode_pod5` -- the GPU transcoder (a HIP device is required; there is no CPU path).
+* :func:`transcode_pod5` -- the GPU transcoder (a HIP device is required; there is no CPU path); with a
+  ``torch.distributed`` group of several ranks (one per GPU) the record batches are shared
+  round-robin, each rank transcodes its share on its GPU (``pgn_pod5_transcode_part``), rank 0
+  gathers the parts and writes the one output file, byte-identical to the one-rank output.
 """
 from __future__ import annotations
 
@@ -21,6 +24,7 @@ import numpy as np
 from . import _native
 
 CONTENT = {0: "reads", 1: "signal", 2: "read_id_index", 3: "other_index", 4: "run_info"}
+PGN_ERR_IO = 13  # include/pgnano_hip.h
 SIGNAL_TYPES = {"uncompressed": 0, "vbz": 1, "pgnano": 2}
 _SIGNAL_NAMES = {v: k for k, v in SIGNAL_TYPES.items()}
 
@@ -89,6 +93,40 @@ class Pod5File:
             raise Pod5FileError(rc, f"read {self.path}")
         return SignalTable(ids, samples, offs, data, self.signal_type)
 
+    def row_columns(self) -> tuple[np.ndarray, np.ndarray]:
+        """(read ids (rows, 16) uint8, samples (rows,) uint32) without the signal column."""
+        ids = np.empty((self.rows, 16), np.uint8)
+        samples = np.empty(self.rows, np.uint32)
+        rc = self._lib.pgn_pod5_signal_read(self._h, _ptr(ids), _ptr(samples), None, None)
+        if rc:
+            raise Pod5FileError(rc, f"read {self.path}")
+        return ids, samples
+
+    def batch_rows(self, batch: int) -> tuple[int, int]:
+        """(first row, rows) of signal record batch `batch`."""
+        r0, n = C.c_uint64(), C.c_uint64()
+        rc = self._lib.pgn_pod5_signal_batch_rows(self._h, int(batch), C.byref(r0), C.byref(n))
+        if rc:
+            raise Pod5FileError(rc, f"batch {batch} of {self.path}")
+        return r0.value, n.value
+
+    def read_batches(self, batch_ids) -> SignalTable:
+        """The rows of the given record batches, in that order (offsets relative to the selection)."""
+        ids_arr = np.ascontiguousarray(batch_ids, np.uint32)
+        rows, nbytes, tot = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        rc = self._lib.pgn_pod5_signal_read_batches(self._h, _ptr(ids_arr), ids_arr.size, C.byref(rows),
+                                                    C.byref(nbytes), C.byref(tot), None, None, None, None)
+        if rc:
+            raise Pod5FileError(rc, f"batches {ids_arr.tolist()} of {self.path}")
+        n = rows.value
+        ids = np.empty((n, 16), np.uint8)
+        samples = np.empty(n, np.uint32)
+        offs = np.empty(n + 1, np.uint64)
+        data = np.empty(nbytes.value, np.uint8)
+        self._lib.pgn_pod5_signal_read_batches(self._h, _ptr(ids_arr), ids_arr.size, None, None, None, _ptr(ids),
+                                               _ptr(samples), offs.ctypes.data, _ptr(data))
+        return SignalTable(ids, samples, offs, data, self.signal_type)
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.pgn_pod5_file_close(self._h)
@@ -134,24 +172,169 @@ class _TranscodeStats(C.Structure):
                 ("decode_ms", C.c_float), ("encode_ms", C.c_float)]
 
 
-def transcode_pod5(in_path: str, out_path: str, dst: str = "pgnano", variant: str = "C5", device: int = 0,
-                   rows_per_batch: int = 100, codec=None) -> dict:
+def _stats_dict(rows, samples, in_bytes, out_bytes, decode_ms, encode_ms) -> dict:
+    n = max(samples, 1)
+    return {"rows": rows, "samples": samples, "in_bytes": in_bytes, "out_bytes": out_bytes,
+            "bits_per_sample": 8.0 * out_bytes / n, "decode_ms": decode_ms, "encode_ms": encode_ms}
+
+
+def transcode_pod5(in_path: str, out_path: str, dst: str = "pgnano", variant: str = "C5", device: int | None = None,
+                   rows_per_batch: int = 100, codec=None, group=None) -> dict:
     """``copy in.pod5 out.pod5 --pgnano`` (dst="pgnano") or ``--VBZ`` (dst="vbz"), or an uncompressed
     signal table (dst="uncompressed"), on the GPU: one batched decode and one batched encode of every
-    row, written with the input's read ids, row order, reads and run-info tables."""
+    row, written with the input's read ids, row order, reads and run-info tables.
+
+    With torch.distributed initialised and more than one rank in `group` (default: the world), every
+    rank must call this with the same arguments: see :func:`transcode_pod5_ranks`.  `device` defaults
+    to 0 (one rank) or LOCAL_RANK (several)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        return transcode_pod5_ranks(in_path, out_path, dst, variant, device, rows_per_batch, codec, group)
     from .codec import PGNanoCodec, PGNanoError
 
     own = codec is None
-    c = codec or PGNanoCodec(device)
+    c = codec or PGNanoCodec(0 if device is None else device)
     try:
         st = _TranscodeStats()
         rc = c._lib.pgn_pod5_transcode_file(c._h, str(in_path).encode(), str(out_path).encode(), SIGNAL_TYPES[dst],
                                             _native.VARIANTS[variant], int(rows_per_batch), C.byref(st))
         if rc:
             raise PGNanoError(rc, c._lib.pgn_pod5_last_error().decode())
-        n = max(st.samples, 1)
-        return {"rows": st.rows, "samples": st.samples, "in_bytes": st.in_bytes, "out_bytes": st.out_bytes,
-                "bits_per_sample": 8.0 * st.out_bytes / n, "decode_ms": st.decode_ms, "encode_ms": st.encode_ms}
+        return _stats_dict(st.rows, st.samples, st.in_bytes, st.out_bytes, st.decode_ms, st.encode_ms)
     finally:
         if own:
             c.close()
+
+
+def _native_part(codec, f: Pod5File, batch_ids, dst: str, variant: str):
+    """This rank's share on its GPU: (status, offsets, data, stats)."""
+    ids = np.ascontiguousarray(batch_ids, np.uint32)
+    st = _TranscodeStats()
+    h = C.c_void_p()
+    lib = codec._lib
+    rc = lib.pgn_pod5_transcode_part(codec._h, f._h, _ptr(ids), ids.size, SIGNAL_TYPES[dst], _native.VARIANTS[variant],
+                                     C.byref(h), C.byref(st))
+    if rc:
+        return rc, lib.pgn_pod5_last_error().decode(errors="replace"), None, None
+    try:
+        rows, po, pd = C.c_uint64(), C.c_void_p(), C.c_void_p()
+        lib.pgn_pod5_part_get(h, C.byref(rows), C.byref(po), C.byref(pd))
+        n = rows.value
+        offs = np.ctypeslib.as_array(C.cast(po, C.POINTER(C.c_uint64)), (n + 1,)).copy()
+        nbytes = int(offs[-1])
+        data = (np.ctypeslib.as_array(C.cast(pd, C.POINTER(C.c_uint8)), (nbytes,)).copy() if nbytes
+                else np.empty(0, np.uint8))
+    finally:
+        lib.pgn_pod5_part_free(h)
+    return 0, (offs, data), [st.rows, st.samples, st.in_bytes, st.out_bytes], [st.decode_ms, st.encode_ms]
+
+
+def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", variant: str = "C5",
+                         device: int | None = None, rows_per_batch: int = 100, codec=None, group=None,
+                         _part=None) -> dict:
+    """Multi-GPU ``copy``: one process per GPU, each rank the same call.
+
+    Record batch b of the input's signal table goes to rank b % W (the reference's reader decodes
+    whole record batches, signal_table_reader.cpp:294-318; its writer takes whole read batches,
+    c_api.cpp:1104-1110), so the ranks share the file with no data exchange until the end.  Each
+    rank transcodes its batches with one batched decode and one batched encode on its GPU; then the
+    ranks all-gather (status, rows, bytes), rank 0 gathers the packed parts, puts the rows back in
+    record-batch order and writes the file exactly as the one-rank call does.  A failure on any rank
+    raises on every rank.  The payload moves over the group's backend (gloo: host tensors; nccl =
+    RCCL: device tensors on this rank's GPU).  Returns the whole job's stats on every rank
+    (decode_ms / encode_ms: the slowest rank's).  `_part` replaces the GPU share (tests on CPU)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    from .codec import PGNanoError
+
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", rank))
+    f = Pod5File(in_path)
+    own = False
+    try:
+        mine = list(range(rank, f.batches, world))
+        if _part is None:
+            from .codec import PGNanoCodec
+
+            own = codec is None
+            codec = codec or PGNanoCodec(device)
+            status, payload, counts, times = _native_part(codec, f, mine, dst, variant)
+        else:
+            status, payload, counts, times = _part(f, mine, dst, variant)
+        nccl = dist.get_backend(group) == "nccl"
+        dev = torch.device("cuda", device) if nccl else torch.device("cpu")
+        if status:
+            counts, times, nbytes = [0, 0, 0, 0], [0.0, 0.0], 0
+        else:
+            offs, data = payload
+            nbytes = 8 * offs.size + data.size
+        head = torch.tensor([status, nbytes] + counts, dtype=torch.int64, device=dev)
+        heads = [torch.empty_like(head) for _ in range(world)]
+        dist.all_gather(heads, head, group=group)
+        tm = torch.tensor(times, dtype=torch.float64, device=dev)
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX, group=group)
+        heads = torch.stack(heads).cpu().numpy()
+        bad = [(r, int(heads[r, 0])) for r in range(world) if heads[r, 0]]
+        if bad:
+            r, s = bad[0]
+            raise PGNanoError(s, payload if r == rank else f"rank {r} failed")
+        # rank 0 gathers every part (padded to the largest) and writes the file
+        cap = int(heads[:, 1].max())
+        buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        if nbytes:
+            mine_bytes = np.concatenate([offs.view(np.uint8), data])
+            buf[:nbytes] = torch.from_numpy(mine_bytes).to(dev)
+        parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+        dist.gather(buf, parts, dst=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        err = None
+        if rank == 0:
+            try:
+                _write_gathered(f, parts, heads, world, out_path, dst, rows_per_batch)
+            except Exception as e:  # every rank learns of it below, instead of waiting in a barrier
+                err = e
+        flag = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
+        dist.broadcast(flag, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if err is not None:
+            raise err
+        if int(flag.item()):
+            raise Pod5FileError(PGN_ERR_IO, f"rank 0 failed to write {out_path}")
+        tot = heads[:, 2:].sum(axis=0)
+        return _stats_dict(int(tot[0]), int(tot[1]), int(tot[2]), int(tot[3]), float(tm[0]), float(tm[1]))
+    finally:
+        if own:
+            codec.close()
+        f.close()
+
+
+def _write_gathered(f: Pod5File, parts, heads, world: int, out_path: str, dst: str, rows_per_batch: int) -> None:
+    """Rank 0: the ranks' parts back in record-batch order, written with the source's other tables."""
+    pieces = []
+    for r in range(world):
+        n = int(heads[r, 2])
+        raw = parts[r][:int(heads[r, 1])].cpu().numpy()
+        po = raw[:8 * (n + 1)].view(np.uint64)
+        pieces.append((po, raw[8 * (n + 1):]))
+    sizes = np.zeros(f.rows, np.uint64)
+    chunks = []
+    at = [0] * world  # next row of each rank's part
+    for b in range(f.batches):
+        r = b % world
+        po, pdata = pieces[r]
+        first, n = f.batch_rows(b)
+        lo, hi = at[r], at[r] + n
+        sizes[first:first + n] = np.diff(po[lo:hi + 1])
+        chunks.append(pdata[int(po[lo]):int(po[hi])])
+        at[r] = hi
+    if at != [int(heads[r, 2]) for r in range(world)]:
+        raise Pod5FileError(PGN_ERR_IO, "gathered parts disagree with the record batches' row counts")
+    offs_all = np.zeros(f.rows + 1, np.uint64)
+    np.cumsum(sizes, out=offs_all[1:])
+    data_all = np.concatenate(chunks) if chunks else np.empty(0, np.uint8)
+    ids, samples = f.row_columns()
+    write_pod5(out_path, SignalTable(ids, samples, offs_all, data_all, dst), source=f,
+               rows_per_batch=rows_per_batch)

@@ -179,3 +179,118 @@ def test_launcher_gives_each_rank_torchrun_env(tmp_path):
     assert {e["WORLD_SIZE"] for e in envs} == {"3"} and {e["MASTER_ADDR"] for e in envs} == {"127.0.0.1"}
     assert len({e["MASTER_PORT"] for e in envs}) == 1
     assert bench.launch_workers(2, [str(tmp_path), "1"], script=probe, timeout=120) == 3
+
+
+# ---- multi-rank POD5 transcode (pod5_file.transcode_pod5_ranks) under gloo ----------------------
+def _oracle_part(f, batch_ids, dst, variant):
+    """CPU stand-in for pgn_pod5_transcode_part: the oracle decodes VBZ and encodes C5 row by row."""
+    import numpy as np
+
+    import _oracle as O
+
+    assert dst == "pgnano" and variant == "C5"
+    t = f.read_batches(batch_ids)
+    blobs = []
+    for i in range(t.rows):
+        rc, x = O.vbz_decompress(t.blob(i), int(t.samples[i]))
+        assert rc == 0
+        rc, blob, _ = O.c5_compress(x)
+        assert rc == 0
+        blobs.append(np.frombuffer(blob, np.uint8))
+    offs = np.zeros(t.rows + 1, np.uint64)
+    np.cumsum([b.size for b in blobs], out=offs[1:])
+    data = np.concatenate(blobs) if blobs else np.empty(0, np.uint8)
+    return 0, (offs, data), [t.rows, int(t.samples.sum()), int(t.offsets[-1]), int(offs[-1])], [1.0, 2.0]
+
+
+def _failing_part(f, batch_ids, dst, variant):
+    if batch_ids and batch_ids[0] == 1:
+        return 11, "synthetic failure", None, None
+    return _oracle_part(f, batch_ids, dst, variant)
+
+
+def _transcode_worker(rank, world, port, src, out, rpb, fail, q):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    sys.path.insert(0, os.path.dirname(here))
+    import torch.distributed as dist
+
+    from rawnanoporesignalcompression_amd import pod5_file as Pm
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = Pm.transcode_pod5_ranks(src, out, "pgnano", "C5", rows_per_batch=rpb,
+                                     _part=_failing_part if fail else _oracle_part)
+        q.put((rank, "ok", st))
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, "error", f"{type(e).__name__}: {e}"))
+    dist.destroy_process_group()
+
+
+def _run_transcode(world, src, out, rpb, fail=False):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_transcode_worker, args=(r, world, port, src, out, rpb, fail, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _unmarked(path):
+    b = open(path, "rb").read()
+    return b.replace(b[8:24], bytes(16))  # the section marker is random per file
+
+
+@pytest.mark.parametrize("world,src_rpb", [(2, 3), (3, 4), (2, 100)])
+def test_multi_rank_transcode_matches_single_rank(tmp_path, world, src_rpb):
+    """Record batches shared round-robin over gloo ranks, gathered on rank 0: the file is the one a
+    single rank writes from the same per-row blobs (byte for byte, section marker aside)."""
+    import numpy as np
+
+    from _golden import HERE as GOLDEN
+    from rawnanoporesignalcompression_amd import pod5_file as Pm
+
+    src = str(tmp_path / "src.pod5")
+    with Pm.Pod5File(os.path.join(GOLDEN, "multi_fast5_zip_v3.pod5")) as f:
+        Pm.write_pod5(src, f.signal_table(), source=f, rows_per_batch=src_rpb)  # several record batches
+    out = str(tmp_path / "multi.pod5")
+    res = _run_transcode(world, src, out, rpb=7)
+    assert all(r[1] == "ok" for r in res), res
+    with Pm.Pod5File(src) as f:
+        assert f.batches == -(-22 // src_rpb)
+        st, (offs, data), counts, _ = _oracle_part(f, list(range(f.batches)), "pgnano", "C5")
+        t = f.signal_table()
+        one = str(tmp_path / "one.pod5")
+        Pm.write_pod5(one, Pm.SignalTable(t.read_ids, t.samples, offs, data, "pgnano"), source=f, rows_per_batch=7)
+    assert _unmarked(out) == _unmarked(one)
+    for _, _, stats in res:
+        assert stats["rows"] == 22 and stats["samples"] == counts[1]
+        assert stats["in_bytes"] == counts[2] and stats["out_bytes"] == counts[3]
+        assert stats["decode_ms"] == 1.0 and stats["encode_ms"] == 2.0
+    with Pm.Pod5File(out) as g:
+        assert g.signal_type == "pgnano" and g.rows == 22 and g.batches == 4
+        np.testing.assert_array_equal(g.signal_table().offsets, offs)
+
+
+def test_multi_rank_transcode_failure_raises_everywhere(tmp_path):
+    from _golden import HERE as GOLDEN
+    from rawnanoporesignalcompression_amd import pod5_file as Pm
+
+    src = str(tmp_path / "src.pod5")
+    with Pm.Pod5File(os.path.join(GOLDEN, "multi_fast5_zip_v3.pod5")) as f:
+        Pm.write_pod5(src, f.signal_table(), source=f, rows_per_batch=3)
+    out = tmp_path / "never.pod5"
+    res = _run_transcode(2, src, str(out), rpb=100, fail=True)
+    assert [r[1] for r in res] == ["error", "error"]
+    assert "synthetic failure" in res[1][2] and "rank 1 failed" in res[0][2]
+    assert not out.exists()

@@ -88,3 +88,27 @@ def test_pgnano_batch_matches_per_chunk_oracle(codec, chunk):
         assert np.array_equal(b.decompress_rows(offsets, data, samples), np.concatenate(reads))
     finally:
         b.close()
+
+
+def test_uniform_noise_chunks_fail_without_fault(codec):
+    """Chunks the codec refuses (uniform noise does not fit pgnano's 2n + 26 bound, compressor.h:39-45)
+    fail the call with PGN_ERR_DST_TOO_SMALL at the first failing chunk; the packing scan skips
+    failed chunks' sizes, so nothing is written out of bounds, and the batch keeps working."""
+    from rawnanoporesignalcompression_amd import PGNanoError, Pod5SignalBatch
+
+    rng = np.random.default_rng(7)
+    good = [O.synth_read(900 + i, 150000) for i in range(6)]
+    noise = [rng.integers(-32768, 32767, 102400 * 3, dtype=np.int16) for _ in range(40)]
+    b = Pod5SignalBatch(codec)
+    try:
+        with pytest.raises(PGNanoError) as e:
+            b.compress_reads(good + noise)
+        assert e.value.status == 1  # PGN_ERR_DST_TOO_SMALL
+        assert "chunk 12" in str(e.value)  # 6 good reads x 2 chunks, then the first noise chunk
+        offsets, data, samples, _ = b.compress_reads(good)
+        assert len(samples) == 12
+        for i in (0, 5, 11):
+            rc, ref, _ = O.c5_compress(good[i // 2][(i % 2) * 102400:(i % 2 + 1) * 102400])
+            assert rc == 0 and data[offsets[i]:offsets[i + 1]].tobytes() == ref
+    finally:
+        b.close()
