@@ -42,7 +42,7 @@ typedef enum pgn_status {
  * or C1 svb16 buffer above 512 KiB (noisy chunks near this limit) is PGN_ERR_UNSUPPORTED.  The
  * reference writer's default chunk is 102,400 samples (pod5/c++/pod5_format/file_writer.h:22) and
  * the chunk size is a writer option (c_api.h:526-539). */
-#define PGN_MAX_CHUNK_SAMPLES 262144u
+#define PGN_MAX_CHUNK_SAMPLES 16777216u
 
 /* Per-chunk statistics, the reference's global byte counters (src/c++/copy.cpp:64-85, updated at
  * C5.hpp:318-324,467-471): raw stream sizes then frame sizes, order keys, S, M, Llow, Lhigh. */

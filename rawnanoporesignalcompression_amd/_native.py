@@ -28,7 +28,7 @@ PGN_ERR_NO_DEVICE = 12
 PGN_ERR_IO = 13
 
 PGN_POD5_CODEC_VBZ = 100  # include/pgnano_pod5.h
-PGN_MAX_CHUNK_SAMPLES = 262144
+PGN_MAX_CHUNK_SAMPLES = 16777216
 # pgn_variant: the reference's compile-time COMPRESSOR_* variants (pgnano.cpp:70-92)
 VARIANTS = {"C5": 0, "C4": 1, "C1": 2, "C2": 3, "C3": 4, "VBZ0": 5}
 PGN_STATS_PER_CHUNK = 10

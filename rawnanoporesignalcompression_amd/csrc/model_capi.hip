@@ -14,7 +14,7 @@ extern "C" {
 // ZSTD_compress(dst, cap, src, n, 1) equivalent; returns size or 0 on error/unsupported.
 size_t z1m_compress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap)
 {
-    if (n > kMaxFrameSrc || cap < compress_bound(n)) return 0;
+    if (n > 0xFFFFFFF0ull || cap < compress_bound(n)) return 0;
     uint32_t* ht = (uint32_t*)calloc((size_t)1 << 15, 4);
     size_t ns = kMaxSrc / 4 + 2;
     Seq* seqs = (Seq*)malloc(ns * sizeof(Seq));

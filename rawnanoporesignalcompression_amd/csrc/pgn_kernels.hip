@@ -12,7 +12,9 @@
 #include <mutex>
 
 #include "../../include/pgnano_hip.h"
+#include "../../include/pgnano_pod5.h"
 #include "pgn_c5.h"
+#include "pgn_internal.h"
 #include "pgn_vbz.h"
 #include "pgn_variants.h"
 #include "pgn_zdec.h"
@@ -20,12 +22,16 @@
 
 namespace pgn {
 
-constexpr uint32_t kMaxSamples = PGN_MAX_CHUNK_SAMPLES;
-constexpr uint32_t kMaxStream = kMaxSamples;            // largest C5 stream (M/Llow/Lhigh <= n)
+// Chunks up to kPassSamples take the batched passes, whose per-chunk buffers are spaced for that
+// many samples; larger ones (up to PGN_MAX_CHUNK_SAMPLES) take the large-chunk pass, whose slot
+// buffers are spaced for the largest chunk of the call (launch_large_*).
+constexpr uint32_t kPassSamples = 262144;
+static_assert(PGN_MAX_CHUNK_SAMPLES >= kPassSamples, "chunk limits");
 // literals and sequences live per zstd block (<= 128 KiB); a frame's blocks reuse them
 constexpr uint32_t kMaxEncSeq = (uint32_t)z1::kMaxSrc / 4 + 2;  // every match covers >= 4 bytes
 constexpr uint32_t kMaxDecSeq = (uint32_t)z1::kMaxSrc / 3 + 2;  // any valid block: matches >= 3 bytes
-static_assert(kMaxStream <= z1::kMaxFrameSrc, "a C5 stream must fit one encoder frame");
+// every stream of the largest chunk fits one encoder frame (its svb16 buffer, ~2.13 n, the largest)
+static_assert((size_t)PGN_MAX_CHUNK_SAMPLES * 9 / 4 + 64 <= kMaxFrameBytes, "frame index field");
 constexpr int kStreams = 5;
 // Codecs of a batch call: the pgnano C5 variant (5 zstd frames per chunk) and the pod5 VBZ codec
 // (one zstd frame per chunk).  Both share the per-chunk buffers and the zstd kernels.
@@ -33,20 +39,26 @@ enum Codec : int { kCodecC5 = 0, kCodecVbz = 1, kCodecC4 = 2, kCodecC1 = 3, kCod
 
 __host__ __device__ constexpr size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-// Capacity of C5 stream s of a chunk of at most kMaxSamples samples: keys n/4, S n/2, M/Ll/Lh n.
-__host__ __device__ constexpr uint32_t stream_cap(int s)
+// Capacity of C5 stream s of a chunk of at most capN samples: keys n/4, S n/2, M/Ll/Lh n.  The
+// stream area of a chunk (3.75 capN) also holds its VBZ / C1 svb16 buffer (<= 2.13 n) and the other
+// variants' streams.
+__host__ __device__ constexpr uint32_t stream_cap(int s, uint32_t capN = kPassSamples)
 {
-    return s == 0 ? kMaxSamples / 4 + 1 : (s == 1 ? kMaxSamples / 2 + 1 : kMaxStream);
+    return s == 0 ? capN / 4 + 1 : (s == 1 ? capN / 2 + 1 : capN);
 }
-__host__ __device__ constexpr size_t stream_pad(int s) { return align_up((size_t)stream_cap(s) + 64, 256); }
+__host__ __device__ constexpr size_t stream_pad(int s, uint32_t capN = kPassSamples)
+{
+    return align_up((size_t)stream_cap(s, capN) + 64, 256);
+}
 // byte offset of stream s inside a chunk's stream area
-__host__ __device__ constexpr size_t stream_off(int s)
+__host__ __device__ constexpr size_t stream_off(int s, uint32_t capN = kPassSamples)
 {
     size_t o = 0;
-    for (int t = 0; t < s; t++) o += stream_pad(t);
+    for (int t = 0; t < s; t++) o += stream_pad(t, capN);
     return o;
 }
-constexpr size_t kChunkStreamBytes = stream_off(kStreams);
+__host__ __device__ constexpr size_t chunk_stream_bytes(uint32_t capN) { return stream_off(kStreams, capN); }
+constexpr size_t kChunkStreamBytes = chunk_stream_bytes(kPassSamples);
 // ZSTD_COMPRESSBOUND (the frame of a stream never exceeds it)
 __host__ __device__ constexpr size_t frame_bound(size_t n)
 {
@@ -103,11 +115,15 @@ __host__ __device__ inline DecLayout dec_layout()
     l.bytes = o;
     return l;
 }
-constexpr size_t kInterCap = (size_t)5 * kMaxStream;
+// A chunk's intermediate (the decoded frames back to back) holds 5 capN bytes: a C5 chunk's five
+// streams (<= 3.75 n), an svb16 buffer with its padding (<= 2.13 n + 16).
+__host__ __device__ constexpr size_t inter_cap(uint32_t capN) { return (size_t)5 * capN; }
 // svb16::decode_input_buffer_padding_byte_count() on x86-64 (svb16/decode.hpp:16-23): the VBZ
 // intermediate is the frame content plus 16 bytes, and ZSTD_decompress may fill them.
 constexpr size_t kVbzPadding = 16;
-constexpr size_t kChunkInterBytes = align_up(kInterCap + 64, 256);
+__host__ __device__ constexpr size_t chunk_inter_bytes(uint32_t capN) { return align_up(inter_cap(capN) + 64, 256); }
+constexpr size_t kInterCap = inter_cap(kPassSamples);
+constexpr size_t kChunkInterBytes = chunk_inter_bytes(kPassSamples);
 
 // Work-unit order of the per-stream kernels: the large streams first (M, S, keys, Llow, Lhigh), so
 // the dynamic queue ends with short units.
@@ -138,6 +154,10 @@ struct EncArgs {
     uint64_t* prof;
     size_t base, G;
     uint32_t nu;         // zstd work units per chunk: 5 (C5) or 1 (VBZ)
+    // fused kernels: slot buffers spaced for capN samples; chunk u of the queue is list[u] (the
+    // large-chunk pass) or u
+    uint32_t capN;
+    const uint32_t* list;
 };
 
 __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
@@ -150,7 +170,7 @@ __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
     P.init(a.prof);
     const uint32_t n = a.sampleCounts[c];
     uint32_t* sz = a.sizes + g * kStreams;
-    if (n > kMaxSamples) {
+    if (n > kPassSamples) {  // the large-chunk pass takes it (or reports it unsupported)
         if (lane_id() == 0) {
             sz[0] = ~0u;
             a.status[c] = PGN_ERR_UNSUPPORTED;
@@ -283,6 +303,8 @@ struct DecArgs {
     uint32_t nu;         // zstd work units per chunk: 5 (C5) or 1 (VBZ)
     uint32_t segCap;     // Huffman segment scratch per slot; 0 = the two-pass decoder (PGN_HUF=twopass)
     uint32_t segDiag;    // PGN_SEG_DIAG (timing experiments)
+    uint32_t capN;       // fused kernels: as EncArgs
+    const uint32_t* list;
 };
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
@@ -310,7 +332,7 @@ __device__ inline int c5_parse_chunk(const uint8_t* in, uint64_t src0, uint64_t 
     }
     uint32_t off = 0;
     for (int s = 0; s < kStreams; s++) {
-        if (cs[s] > kMaxStream) return PGN_ERR_UNSUPPORTED;
+        if (cs[s] > kPassSamples) return PGN_ERR_UNSUPPORTED;
         u[s].cs = (uint32_t)cs[s];
         u[s].interOff = off;
         off += (uint32_t)cs[s];
@@ -323,7 +345,9 @@ __global__ __launch_bounds__(64) void dec_parse_kernel(DecArgs a)
     const size_t g = (size_t)blockIdx.x * 64 + lane_id();
     const size_t c = a.base + g;
     if (g >= a.G || c >= a.nchunks) return;
-    a.status[c] = c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], a.units + g * kStreams);
+    // a chunk above kPassSamples is left to the large-chunk pass
+    a.status[c] = a.sampleCounts[c] > kPassSamples ? PGN_ERR_UNSUPPORTED
+                                                   : c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], a.units + g * kStreams);
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void dec_zstd_kernel(DecArgs a)
@@ -406,7 +430,7 @@ __global__ __launch_bounds__(64) void vbz_split_kernel(EncArgs a)
     P.init(a.prof);
     const uint32_t n = a.sampleCounts[c];
     uint32_t* sz = a.sizes + g * kStreams;
-    if (n > kMaxSamples) {
+    if (n > kPassSamples) {  // the large-chunk pass takes it
         if (lane_id() == 0) {
             sz[0] = ~0u;
             a.status[c] = PGN_ERR_UNSUPPORTED;
@@ -418,14 +442,8 @@ __global__ __launch_bounds__(64) void vbz_split_kernel(EncArgs a)
     const uint32_t pad = (16u - (svb_key_length(n) & 15u)) & 15u;
     const uint32_t m = vbz_split_wave(a.samples + a.sampleOffsets[c], n, a.streams + g * kChunkStreamBytes + pad, W);
     if (lane_id() == 0) {
-        if (m > z1::kMaxFrameSrc) {  // larger than one single-segment level-1 frame here
-            sz[0] = ~0u;
-            a.status[c] = PGN_ERR_UNSUPPORTED;
-            a.outSizes[c] = 0;
-        } else {
-            sz[0] = m;
-            sz[1] = pad;
-        }
+        sz[0] = m;
+        sz[1] = pad;
     }
     P.mark(0);
     P.flush();
@@ -466,7 +484,8 @@ __global__ __launch_bounds__(64) void vbz_parse_kernel(DecArgs a)
     const uint64_t src0 = a.inOffsets[c], len = a.inSizes[c];
     const uint64_t cs = z1::frame_content_size(a.in + src0, (size_t)len, &ok);
     int st = PGN_OK;
-    if (!ok) st = PGN_ERR_NOT_ZSTD;
+    if (a.sampleCounts[c] > kPassSamples) st = PGN_ERR_UNSUPPORTED;  // the large-chunk pass takes it
+    else if (!ok) st = PGN_ERR_NOT_ZSTD;
     else if (cs + kVbzPadding > kInterCap || len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
     else {
         u->src = src0;
@@ -536,12 +555,16 @@ __host__ __device__ constexpr int codec_frames(int codec)
     return codec == kCodecC5 || codec == kCodecC4 ? 5 : (codec == kCodecC3 ? 4 : (codec == kCodecC2 ? 3 : (codec == kCodecC1 ? 2 : 1)));
 }
 
-// slot scratch of the fused kernels: the zstd scratch, then the chunk's streams (encode: + one
-// frame for a stream that may not fit the destination) or its intermediate (decode)
-// (the frame buffer holds any one stream's frame: a VBZ / C1 svb16 buffer can reach kMaxFrameSrc)
-constexpr size_t kSlotFrameBytes = align_up(frame_bound(z1::kMaxFrameSrc) + 64, 256);
-__host__ __device__ inline size_t enc_slot_bytes() { return enc_layout().bytes + kChunkStreamBytes + kSlotFrameBytes; }
-__host__ __device__ inline size_t dec_slot_bytes() { return dec_layout().bytes + kChunkInterBytes; }
+// slot scratch of the fused kernels for chunks of up to capN samples: the zstd scratch, then the
+// chunk's streams (encode: + one frame for a stream that may not fit the destination; any one
+// stream's frame, a VBZ / C1 svb16 buffer of up to ~2.13 capN the largest) or its intermediate
+// (decode)
+__host__ __device__ inline size_t slot_frame_bytes(uint32_t capN) { return align_up(frame_bound((size_t)capN * 9 / 4 + 64) + 64, 256); }
+__host__ __device__ inline size_t enc_slot_bytes(uint32_t capN = kPassSamples)
+{
+    return enc_layout().bytes + chunk_stream_bytes(capN) + slot_frame_bytes(capN);
+}
+__host__ __device__ inline size_t dec_slot_bytes(uint32_t capN = kPassSamples) { return dec_layout().bytes + chunk_inter_bytes(capN); }
 
 // The split and merge stages as non-inlined calls with wave-uniform arguments: each gets its own
 // register allocation instead of sharing the kernel's with the state kept across the zstd calls
@@ -550,26 +573,28 @@ struct SplitOut {
     uint32_t s[kStreams];
 };
 template <bool C4>
-__device__ __noinline__ SplitOut c5_split_chunk(const int16_t* x, uint32_t n, uint8_t* streams)
+__device__ __noinline__ SplitOut c5_split_chunk(const int16_t* x, uint32_t n, uint8_t* streams, uint32_t capN)
 {
     x = uni(x);
     n = uni(n);
     streams = uni(streams);
-    C5Streams st{streams + stream_off(0), streams + stream_off(1), streams + stream_off(2), streams + stream_off(3),
-                 streams + stream_off(4)};
+    capN = uni(capN);
+    C5Streams st{streams + stream_off(0, capN), streams + stream_off(1, capN), streams + stream_off(2, capN),
+                 streams + stream_off(3, capN), streams + stream_off(4, capN)};
     SplitOut o;
     c5_split_wave<C4>(x, n, st, o.s, *reinterpret_cast<SplitLds*>(&sEnc));
     return o;
 }
 template <bool C3>
-__device__ __noinline__ SplitOut c23_split_chunk(const int16_t* x, uint32_t n, uint8_t* streams)
+__device__ __noinline__ SplitOut c23_split_chunk(const int16_t* x, uint32_t n, uint8_t* streams, uint32_t capN)
 {
     x = uni(x);
     n = uni(n);
     streams = uni(streams);
+    capN = uni(capN);
     SplitOut o;
-    c23_split_wave<C3>(x, n, streams + stream_off(0), streams + stream_off(2), streams + stream_off(3),
-                       streams + stream_off(4), o.s);
+    c23_split_wave<C3>(x, n, streams + stream_off(0, capN), streams + stream_off(2, capN), streams + stream_off(3, capN),
+                       streams + stream_off(4, capN), o.s);
     return o;
 }
 __device__ __noinline__ uint32_t vbz_split_chunk(const int16_t* x, uint32_t n, uint8_t* out)
@@ -642,8 +667,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
     S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
     S.maxSeq = kMaxEncSeq;
     S.huf = (uint32_t*)(sbase + lay.huf);
+    const uint32_t capN = a.capN;
     uint8_t* streams = sbase + lay.bytes;
-    uint8_t* fbuf = streams + kChunkStreamBytes;
+    uint8_t* fbuf = streams + chunk_stream_bytes(capN);
     uint32_t epoch = a.epochs[blockIdx.x];  // table state: epoch tag | written extent << 8 (ht_next_epoch)
     PhaseProf P;
     P.init(a.prof);
@@ -652,9 +678,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
         if (lane == 0) u = atomicAdd(a.queue, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= a.nchunks) break;
-        const size_t c = u;
+        const size_t c = a.list ? a.list[u] : u;
         const uint32_t n = a.sampleCounts[c];
-        if (n > kMaxSamples) {
+        if (n > capN) {  // the large-chunk pass takes it (or reports it unsupported)
             enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
             continue;
         }
@@ -676,26 +702,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
         } else if (Codec == kCodecVbz0) {
             sz[0] = vbz0_split_chunk(x, n, streams);
         } else if (Codec == kCodecC2 || Codec == kCodecC3) {
-            const SplitOut so = c23_split_chunk<Codec == kCodecC3>(x, n, streams);
+            const SplitOut so = c23_split_chunk<Codec == kCodecC3>(x, n, streams, capN);
 #pragma unroll
             for (int s = 0; s < kStreams; s++) sz[s] = so.s[s];
-            src[0] = streams + stream_off(0);
-            src[1] = streams + stream_off(2);
-            src[2] = streams + stream_off(Codec == kCodecC3 ? 3 : 4);
-            src[3] = streams + stream_off(4);
+            src[0] = streams + stream_off(0, capN);
+            src[1] = streams + stream_off(2, capN);
+            src[2] = streams + stream_off(Codec == kCodecC3 ? 3 : 4, capN);
+            src[3] = streams + stream_off(4, capN);
         } else {
-            const SplitOut so = c5_split_chunk<Codec == kCodecC4>(x, n, streams);
+            const SplitOut so = c5_split_chunk<Codec == kCodecC4>(x, n, streams, capN);
 #pragma unroll
             for (int s = 0; s < kStreams; s++) {
                 sz[s] = so.s[s];
-                src[s] = streams + stream_off(s);
+                src[s] = streams + stream_off(s, capN);
             }
         }
 #pragma unroll
         for (int s = 0; s < kStreams; s++) sz[s] = uni(sz[s]);
-        bool big = false;  // a stream above one single-segment frame (512 KiB): not on the GPU encoder
+        bool big = false;  // a stream above the encoder's largest frame (not reached below the chunk limit)
 #pragma unroll
-        for (int s = 0; s < nf; s++) big |= sz[s] > z1::kMaxFrameSrc;
+        for (int s = 0; s < nf; s++) big |= sz[s] > kMaxFrameBytes;
         if (big) {
             enc_fail_chunk(a, c, PGN_ERR_UNSUPPORTED);
             continue;
@@ -755,7 +781,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
 // frame records with content sizes and intermediate offsets; the frames together must fit the
 // slot's intermediate.
 template <int NF>
-__device__ inline int parse_frames(const uint8_t* in, uint64_t src0, uint64_t len, DecUnit* u, uint64_t* total)
+__device__ inline int parse_frames(const uint8_t* in, uint64_t src0, uint64_t len, DecUnit* u, uint64_t* total,
+                                   size_t interCap)
 {
     const uint8_t* src = in + src0;
     uint64_t pos = 0, cs[kStreams];
@@ -779,7 +806,7 @@ __device__ inline int parse_frames(const uint8_t* in, uint64_t src0, uint64_t le
     }
     uint64_t off = 0;
     for (int s = 0; s < NF; s++) {
-        if (cs[s] > kInterCap - kVbzPadding - off) return PGN_ERR_UNSUPPORTED;
+        if (cs[s] > interCap - kVbzPadding - off) return PGN_ERR_UNSUPPORTED;
         u[s].cs = (uint32_t)cs[s];
         u[s].interOff = (uint32_t)off;
         off += cs[s];
@@ -805,6 +832,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.segCap = a.segCap;
     S.segDiag = a.segDiag;
     uint8_t* inter = sbase + lay.bytes;
+    const uint32_t capN = a.capN;
     PhaseProf P;
     P.init(a.prof);
     while (true) {
@@ -812,16 +840,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
         if (lane == 0) u = atomicAdd(a.queue, 1u);
         u = __builtin_amdgcn_readfirstlane(u);
         if (u >= a.nchunks) break;
-        const size_t c = u;
+        const size_t c = a.list ? a.list[u] : u;
         const uint32_t n = a.sampleCounts[c];
         int16_t* out = a.samples + a.sampleOffsets[c];
         DecUnit d[kStreams];
         uint64_t total = 0;
-        int st = __builtin_amdgcn_readfirstlane(parse_frames<nf>(a.in, a.inOffsets[c], a.inSizes[c], d, &total));
+        int st = n > capN ? PGN_ERR_UNSUPPORTED  // the large-chunk pass takes it
+                          : __builtin_amdgcn_readfirstlane(
+                                parse_frames<nf>(a.in, a.inOffsets[c], a.inSizes[c], d, &total, inter_cap(capN)));
         if (Codec == kCodecC5 && st == PGN_OK) {  // C5: the staged path's per-stream bound
 #pragma unroll
             for (int s = 0; s < nf; s++)
-                if (d[s].cs > kMaxStream) st = PGN_ERR_UNSUPPORTED;
+                if (d[s].cs > capN) st = PGN_ERR_UNSUPPORTED;
         }
         if (st == PGN_OK) {
 #pragma unroll
@@ -941,6 +971,19 @@ __global__ void synth_tasks_kernel(const uint32_t* counts, size_t nreads, uint64
         taskCount[r] = (counts[r] + 63u) / 64u;
 }
 
+// The chunks above kPassSamples of a batch (their indices, in any order), their count and the
+// largest sample count: hdr = {count, max}, zeroed by the caller.
+__global__ void large_scan_kernel(const uint32_t* counts, size_t n, uint32_t* list, uint32_t* hdr)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint32_t v = counts[i];
+        if (v > kPassSamples) {
+            list[atomicAdd(hdr, 1u)] = (uint32_t)i;
+            atomicMax(hdr + 1, v);
+        }
+    }
+}
+
 }  // namespace pgn
 
 // =============================================================================================
@@ -997,6 +1040,20 @@ struct pgn_ctx {
     // order on the device even when callers pass different streams.
     hipEvent_t evLast = nullptr;
     bool haveLast = false;
+    // Large-chunk pass (chunks above kPassSamples, launch_large): the chunk list, its header
+    // {count, largest} on the device and in pinned memory, read on a stream of its own while the
+    // batched pass runs; slot scratch spaced for the largest chunk, and its own table epochs and
+    // work counter.
+    uint32_t* largeList = nullptr;
+    size_t largeListCap = 0;
+    uint32_t* largeHdr = nullptr;      // [0..1] header, [2] the large pass's work counter
+    uint32_t* largeHdrHost = nullptr;
+    hipStream_t scanStream = nullptr;
+    hipEvent_t evScanFork = nullptr, evScan = nullptr;
+    uint8_t* largeScratch = nullptr;
+    size_t largeScratchBytes = 0;
+    uint32_t* largeEpochs = nullptr;
+    size_t largeEpochSlots = 0;
     std::mutex mu;
 };
 
@@ -1098,6 +1155,11 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
     HIPCHK(hipEventCreateWithFlags(&c->evLast, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->scanStream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->evScanFork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->evScan, hipEventDisableTiming));
+    HIPCHK(hipMalloc(&c->largeHdr, 4 * sizeof(uint32_t)));
+    HIPCHK(hipHostMalloc((void**)&c->largeHdrHost, 4 * sizeof(uint32_t), hipHostMallocDefault));
     HIPCHK(hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming));
     for (int i = 0; i < 2; i++) {
@@ -1128,6 +1190,15 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->queues);
     (void)hipFree(c->stage);
     (void)hipFree(c->prof);
+    if (c->scanStream) (void)hipStreamSynchronize(c->scanStream);
+    (void)hipFree(c->largeList);
+    (void)hipFree(c->largeHdr);
+    (void)hipFree(c->largeScratch);
+    (void)hipFree(c->largeEpochs);
+    if (c->largeHdrHost) (void)hipHostFree(c->largeHdrHost);
+    for (hipEvent_t e : {c->evScanFork, c->evScan})
+        if (e) (void)hipEventDestroy(e);
+    if (c->scanStream) (void)hipStreamDestroy(c->scanStream);
     for (int i = 0; i < 4; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->evLast) (void)hipEventSynchronize(c->evLast);
@@ -1212,6 +1283,9 @@ static int ensure_queues(pgn_ctx* c, size_t n, hipStream_t s)
     return PGN_OK;
 }
 
+static int launch_enc_chunks(int codec, const EncArgs& a, size_t slots, hipStream_t s);
+static int launch_dec_chunks(int codec, const DecArgs& a, size_t slots, hipStream_t s);
+
 static int launch_encode_fused(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples,
                                const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, uint8_t* d_out,
                                const uint64_t* d_out_offsets, const uint64_t* d_out_caps, uint64_t* d_out_sizes,
@@ -1239,6 +1313,13 @@ static int launch_encode_fused(pgn_ctx* c, int codec, size_t nchunks, const int1
     a.epochs = c->epochs;
     a.prof = c->prof;
     a.queue = c->queues;
+    a.capN = kPassSamples;
+    a.list = nullptr;
+    return launch_enc_chunks(codec, a, slots, s);
+}
+
+static int launch_enc_chunks(int codec, const EncArgs& a, size_t slots, hipStream_t s)
+{
     switch (codec) {
     case kCodecC5: hipLaunchKernelGGL(enc_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
     case kCodecVbz: hipLaunchKernelGGL(enc_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
@@ -1250,8 +1331,6 @@ static int launch_encode_fused(pgn_ctx* c, int codec, size_t nchunks, const int1
     default: return PGN_ERR_INVALID_ARG;
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], s));
-    c->encTimed = true;
     return PGN_OK;
 }
 
@@ -1280,7 +1359,14 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     a.queue = c->queues;
     a.segCap = c->hufSegCap;
     a.segDiag = c->segDiag;
+    a.capN = kPassSamples;
+    a.list = nullptr;
     c->lastUnits = nullptr;
+    return launch_dec_chunks(codec, a, slots, s);
+}
+
+static int launch_dec_chunks(int codec, const DecArgs& a, size_t slots, hipStream_t s)
+{
     switch (codec) {
     case kCodecC5: hipLaunchKernelGGL(dec_chunk_kernel<kCodecC5>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
     case kCodecVbz: hipLaunchKernelGGL(dec_chunk_kernel<kCodecVbz>, dim3((unsigned)slots), dim3(64), 0, s, a); break;
@@ -1292,8 +1378,6 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     default: return PGN_ERR_INVALID_ARG;
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[3], s));
-    c->decTimed = true;
     return PGN_OK;
 }
 
@@ -1338,6 +1422,8 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
     a.prof = c->prof;
     a.G = G;
     a.nu = nu;
+    a.capN = kPassSamples;
+    a.list = nullptr;
     // pass p: split on the side stream into buffer p % 2; zstd + assemble on the caller's stream.
     // The split of pass p+1 overlaps the zstd kernel of pass p; a buffer is split into again only
     // after the assemble kernel of the pass before last has read it.
@@ -1361,8 +1447,6 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
         HIPCHK(hipEventRecord(c->evFree[b], s));
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[1], s));
-    c->encTimed = true;
     return PGN_OK;
 }
 
@@ -1404,6 +1488,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.nu = nu;
     a.segCap = c->hufSegCap;
     a.segDiag = c->segDiag;
+    a.capN = kPassSamples;
+    a.list = nullptr;
     // pass p: parse + zstd on the caller's stream into buffer p % 2, merge on the side stream.  The
     // merge of pass p overlaps the zstd kernel of pass p+1; a buffer is parsed into again only after
     // the merge of the pass before last has read it.
@@ -1428,23 +1514,173 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->evJoin, c->side));
     HIPCHK(hipStreamWaitEvent(s, c->evJoin, 0));
-    HIPCHK(hipEventRecord(c->ev[3], s));
-    c->decTimed = true;
     return PGN_OK;
 }
 
+// ---- the large-chunk pass --------------------------------------------------------------------
+// A call whose chunks may exceed kPassSamples (maxHint = the caller's bound on the sample counts,
+// 0 = unknown) lists them on the scan stream, after the work queued before the call, while the
+// batched pass runs (which leaves them UNSUPPORTED); the host reads the list's header and, when it
+// is not empty, runs the fused kernel over the listed chunks with slot buffers spaced for the
+// largest of them.  Chunks above PGN_MAX_CHUNK_SAMPLES stay UNSUPPORTED.
+static bool need_scan(uint32_t maxHint) { return maxHint == 0 || maxHint > kPassSamples; }
+
+static int start_scan(pgn_ctx* c, size_t nchunks, const uint32_t* d_counts, hipStream_t s)
+{
+    if (nchunks > c->largeListCap) {
+        wait_last_host(c);
+        (void)hipStreamSynchronize(c->scanStream);
+        (void)hipFree(c->largeList);
+        c->largeList = nullptr;
+        const size_t m = nchunks < 4096 ? 4096 : nchunks;
+        HIPCHK(hipMalloc(&c->largeList, 4 * m));
+        c->largeListCap = m;
+    }
+    HIPCHK(hipEventRecord(c->evScanFork, s));
+    HIPCHK(hipStreamWaitEvent(c->scanStream, c->evScanFork, 0));
+    HIPCHK(hipMemsetAsync(c->largeHdr, 0, 2 * sizeof(uint32_t), c->scanStream));
+    unsigned grid = (unsigned)((nchunks + 255) / 256);
+    grid = grid > 1024 ? 1024 : grid;
+    hipLaunchKernelGGL(large_scan_kernel, dim3(grid), dim3(256), 0, c->scanStream, d_counts, nchunks, c->largeList,
+                       c->largeHdr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->largeHdrHost, c->largeHdr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->scanStream));
+    HIPCHK(hipEventRecord(c->evScan, c->scanStream));
+    return PGN_OK;
+}
+
+// slot buffers of the large pass: spaced for the largest listed chunk (64 Ki-sample steps, so that
+// similar calls reuse them), as many slots as fit kLargeScratchBudget (at least one)
+constexpr size_t kLargeScratchBudget = (size_t)8 << 30;
+static uint32_t large_cap(uint32_t maxN)
+{
+    const uint64_t r = ((uint64_t)maxN + 65535u) & ~(uint64_t)65535u;
+    return r > PGN_MAX_CHUNK_SAMPLES ? PGN_MAX_CHUNK_SAMPLES : (uint32_t)r;
+}
+static int ensure_large(pgn_ctx* c, size_t bytes, size_t epochSlots)
+{
+    if (bytes > c->largeScratchBytes || epochSlots > c->largeEpochSlots) {
+        wait_last_host(c);
+        (void)hipFree(c->largeScratch);
+        (void)hipFree(c->largeEpochs);
+        c->largeScratch = nullptr;
+        c->largeEpochs = nullptr;
+        c->largeScratchBytes = c->largeEpochSlots = 0;
+        HIPCHK(hipMalloc(&c->largeScratch, bytes));
+        HIPCHK(hipMalloc(&c->largeEpochs, 4 * epochSlots));
+        // fresh tables: tag 0 never matches (as in ensure_enc)
+        HIPCHK(hipMemsetAsync(c->largeEpochs, 0, 4 * epochSlots, c->stream));
+        HIPCHK(hipMemsetAsync(c->largeScratch, 0, bytes, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->largeScratchBytes = bytes;
+        c->largeEpochSlots = epochSlots;
+    }
+    return PGN_OK;
+}
+static size_t large_slots(pgn_ctx* c, uint32_t count, size_t slotBytes, size_t fusedMax)
+{
+    size_t slots = count < fusedMax ? count : fusedMax;
+    if (slots * slotBytes > kLargeScratchBudget) slots = kLargeScratchBudget / slotBytes;
+    return slots ? slots : 1;
+}
+
+static int finish_scan(pgn_ctx* c, uint32_t& count, uint32_t& maxN)
+{
+    HIPCHK(hipEventSynchronize(c->evScan));
+    count = c->largeHdrHost[0];
+    maxN = c->largeHdrHost[1];
+    return PGN_OK;
+}
+
+static int launch_large_encode(pgn_ctx* c, int codec, uint32_t count, uint32_t maxN, size_t nchunks,
+                               const int16_t* d_samples, const uint64_t* d_sample_offsets,
+                               const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
+                               const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
+                               hipStream_t s)
+{
+    const uint32_t capN = large_cap(maxN);
+    const size_t sb = enc_slot_bytes(capN);
+    const size_t slots = large_slots(c, count, sb, c->encFusedSlotsMax);
+    int rc = ensure_large(c, sb * slots, slots);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(c->largeHdr + 2, 0, sizeof(uint32_t), s));
+    EncArgs a{};
+    a.nchunks = count;
+    a.samples = d_samples;
+    a.sampleOffsets = d_sample_offsets;
+    a.sampleCounts = d_sample_counts;
+    a.out = d_out;
+    a.outOffsets = d_out_offsets;
+    a.outCaps = d_out_caps;
+    a.outSizes = d_out_sizes;
+    a.status = d_status;
+    a.stats = d_stats;
+    a.slotScratch = c->largeScratch;
+    a.slotBytes = sb;
+    a.epochs = c->largeEpochs;
+    a.prof = c->prof;
+    a.queue = c->largeHdr + 2;
+    a.capN = capN;
+    a.list = c->largeList;
+    (void)nchunks;
+    return launch_enc_chunks(codec, a, slots, s);
+}
+
+static int launch_large_decode(pgn_ctx* c, int codec, uint32_t count, uint32_t maxN, const uint8_t* d_in,
+                               const uint64_t* d_in_offsets, const uint64_t* d_in_sizes, int16_t* d_samples,
+                               const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, int32_t* d_status,
+                               hipStream_t s)
+{
+    const uint32_t capN = large_cap(maxN);
+    const size_t sb = dec_slot_bytes(capN);
+    const size_t slots = large_slots(c, count, sb, c->decFusedSlotsMax);
+    int rc = ensure_large(c, sb * slots, 0);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(c->largeHdr + 2, 0, sizeof(uint32_t), s));
+    DecArgs a{};
+    a.nchunks = count;
+    a.in = d_in;
+    a.inOffsets = d_in_offsets;
+    a.inSizes = d_in_sizes;
+    a.samples = d_samples;
+    a.sampleOffsets = d_sample_offsets;
+    a.sampleCounts = d_sample_counts;
+    a.status = d_status;
+    a.slotScratch = c->largeScratch;
+    a.slotBytes = sb;
+    a.prof = c->prof ? c->prof + kPhases : nullptr;
+    a.queue = c->largeHdr + 2;
+    a.segCap = c->hufSegCap;
+    a.segDiag = c->segDiag;
+    a.capN = capN;
+    a.list = c->largeList;
+    return launch_dec_chunks(codec, a, slots, s);
+}
+
 // Every launch sequence on a context: ordered after the previous one (evLast, whatever its stream),
-// and recorded as the new last one.
+// and recorded as the new last one.  ev[0..1] / ev[2..3] bracket the call's kernels.
 static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
                          const uint32_t* d_sample_counts, uint8_t* d_out, const uint64_t* d_out_offsets,
                          const uint64_t* d_out_caps, uint64_t* d_out_sizes, int32_t* d_status, uint64_t* d_stats,
-                         void* stream)
+                         void* stream, uint32_t maxHint)
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->haveLast) HIPCHK(hipStreamWaitEvent(s, c->evLast, 0));
-    const int rc = launch_encode_impl(c, codec, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out,
-                                      d_out_offsets, d_out_caps, d_out_sizes, d_status, d_stats, s);
+    const bool scan = need_scan(maxHint);
+    int rc = scan ? start_scan(c, nchunks, d_sample_counts, s) : PGN_OK;
+    if (rc == PGN_OK)
+        rc = launch_encode_impl(c, codec, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
+                                d_out_caps, d_out_sizes, d_status, d_stats, s);
+    uint32_t count = 0, maxN = 0;
+    if (rc == PGN_OK && scan) rc = finish_scan(c, count, maxN);
+    if (rc == PGN_OK && count)
+        rc = launch_large_encode(c, codec, count, maxN, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out,
+                                 d_out_offsets, d_out_caps, d_out_sizes, d_status, d_stats, s);
+    if (rc == PGN_OK) {
+        HIPCHK(hipEventRecord(c->ev[1], s));
+        c->encTimed = true;
+    }
     HIPCHK(hipEventRecord(c->evLast, s));
     c->haveLast = true;
     return rc;
@@ -1452,13 +1688,25 @@ static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d
 
 static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
                          const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
-                         const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
+                         const uint32_t* d_sample_counts, int32_t* d_status, void* stream, uint32_t maxHint)
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->haveLast) HIPCHK(hipStreamWaitEvent(s, c->evLast, 0));
-    const int rc = launch_decode_impl(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
-                                      d_sample_counts, d_status, s);
+    const bool scan = need_scan(maxHint);
+    int rc = scan ? start_scan(c, nchunks, d_sample_counts, s) : PGN_OK;
+    if (rc == PGN_OK)
+        rc = launch_decode_impl(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                                d_sample_counts, d_status, s);
+    uint32_t count = 0, maxN = 0;
+    if (rc == PGN_OK && scan) rc = finish_scan(c, count, maxN);
+    if (rc == PGN_OK && count)
+        rc = launch_large_decode(c, codec, count, maxN, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                                 d_sample_counts, d_status, s);
+    if (rc == PGN_OK) {
+        HIPCHK(hipEventRecord(c->ev[3], s));
+        c->decTimed = true;
+    }
     HIPCHK(hipEventRecord(c->evLast, s));
     c->haveLast = true;
     return rc;
@@ -1467,7 +1715,7 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
 static int compress_batch(int codec, pgn_ctx* c, size_t nchunks, const int16_t* d_samples,
                           const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, uint8_t* d_out,
                           const uint64_t* d_out_offsets, const uint64_t* d_out_caps, uint64_t* d_out_sizes,
-                          int32_t* d_status, uint64_t* d_stats, void* stream)
+                          int32_t* d_status, uint64_t* d_stats, void* stream, uint32_t maxHint = 0)
 {
     if (!c || !d_samples || !d_sample_offsets || !d_sample_counts || !d_out || !d_out_offsets || !d_out_caps ||
         !d_out_sizes || !d_status)
@@ -1475,19 +1723,19 @@ static int compress_batch(int codec, pgn_ctx* c, size_t nchunks, const int16_t* 
     if (nchunks == 0) return PGN_OK;
     std::lock_guard<std::mutex> g(c->mu);
     return launch_encode(c, codec, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets, d_out_caps,
-                         d_out_sizes, d_status, d_stats, stream);
+                         d_out_sizes, d_status, d_stats, stream, maxHint);
 }
 
 static int decompress_batch(int codec, pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
                             const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
-                            const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
+                            const uint32_t* d_sample_counts, int32_t* d_status, void* stream, uint32_t maxHint = 0)
 {
     if (!c || !d_in || !d_in_offsets || !d_in_sizes || !d_samples || !d_sample_offsets || !d_sample_counts || !d_status)
         return PGN_ERR_INVALID_ARG;
     if (nchunks == 0) return PGN_OK;
     std::lock_guard<std::mutex> g(c->mu);
     return launch_decode(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets, d_sample_counts,
-                         d_status, stream);
+                         d_status, stream, maxHint);
 }
 
 int pgn_compress_batch_device(pgn_ctx* c, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
@@ -1559,6 +1807,37 @@ int pgn_variant_decompress_batch_device(pgn_ctx* c, int variant, size_t nchunks,
     return decompress_batch(codec, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                             d_sample_counts, d_status, stream);
 }
+
+}  // extern "C"
+
+static int bounded_codec(int codec)
+{
+    return codec == PGN_POD5_CODEC_VBZ ? (int)kCodecVbz : variant_codec(codec);
+}
+
+int pgn_compress_batch_bounded(pgn_ctx* c, int codec, uint32_t max_samples, size_t nchunks, const int16_t* d_samples,
+                               const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, uint8_t* d_out,
+                               const uint64_t* d_out_offsets, const uint64_t* d_out_caps, uint64_t* d_out_sizes,
+                               int32_t* d_status, uint64_t* d_stats, void* stream)
+{
+    const int k = bounded_codec(codec);
+    if (k < 0) return PGN_ERR_INVALID_ARG;
+    return compress_batch(k, c, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets, d_out_caps,
+                          d_out_sizes, d_status, d_stats, stream, max_samples);
+}
+
+int pgn_decompress_batch_bounded(pgn_ctx* c, int codec, uint32_t max_samples, size_t nchunks, const uint8_t* d_in,
+                                 const uint64_t* d_in_offsets, const uint64_t* d_in_sizes, int16_t* d_samples,
+                                 const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, int32_t* d_status,
+                                 void* stream)
+{
+    const int k = bounded_codec(codec);
+    if (k < 0) return PGN_ERR_INVALID_ARG;
+    return decompress_batch(k, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets, d_sample_counts,
+                            d_status, stream, max_samples);
+}
+
+extern "C" {
 
 #ifdef PGN_DEBUG_HUF
 // diagnostic build only: the Huffman decoder's record buffer (count, then records of 8 words)
@@ -1683,7 +1962,7 @@ static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t
                            size_t* out_size)
 {
     if (!c || (!samples && n) || !dst || !out_size) return PGN_ERR_INVALID_ARG;
-    if (n > kMaxSamples) return PGN_ERR_UNSUPPORTED;
+    if (n > PGN_MAX_CHUNK_SAMPLES) return PGN_ERR_UNSUPPORTED;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     const size_t hdrB = 256, inB = align_up(2 * n + 16, 256);
@@ -1701,7 +1980,7 @@ static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t
     if (n) HIPCHK(hipMemcpyAsync(din, samples, 2 * n, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
     rc = launch_encode(c, codec, 1, (const int16_t*)din, &d->off0, &d->count, dout, &d->outOff, &d->outCap,
-                                   &d->outSize, &d->status, d->stats, c->stream);
+                       &d->outSize, &d->status, d->stats, c->stream, n ? (uint32_t)n : 1u);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(&h, dh, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1714,7 +1993,7 @@ static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t
 static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
 {
     if (!c || (!src && len) || (!dst && n)) return PGN_ERR_INVALID_ARG;
-    if (n > kMaxSamples) return PGN_ERR_UNSUPPORTED;
+    if (n > PGN_MAX_CHUNK_SAMPLES) return PGN_ERR_UNSUPPORTED;
     const size_t hdrB = 256, inB = align_up(len + 16, 256);
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
@@ -1731,8 +2010,8 @@ static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t l
     HIPCHK(hipMemcpyAsync(dh, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
     if (len) HIPCHK(hipMemcpyAsync(din, src, len, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
-    rc = launch_decode(c, codec, 1, din, &d->inOff, &d->inSize, dout, &d->off0, &d->count, &d->status,
-                                         c->stream);
+    rc = launch_decode(c, codec, 1, din, &d->inOff, &d->inSize, dout, &d->off0, &d->count, &d->status, c->stream,
+                       n ? (uint32_t)n : 1u);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(&h, dh, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

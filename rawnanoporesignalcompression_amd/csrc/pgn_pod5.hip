@@ -20,6 +20,7 @@
 
 #include "../../include/pgnano_pod5.h"
 #include "../../include/pgnano_pod5file.h"
+#include "pgn_internal.h"
 
 namespace {
 
@@ -273,26 +274,22 @@ static uint64_t chunk_cap(int codec, uint32_t n)
                                        : (uint64_t)pgn_compressed_signal_max_size(n);
 }
 
+// maxN: the largest sample count of the call's chunks (known on the host here: no large-chunk scan
+// unless a chunk needs the large pass)
 static int batch_compress(pgn_pod5_batch* b, size_t n, const int16_t* d_samples, const uint64_t* d_soff,
                           const uint32_t* d_cnt, uint8_t* d_out, const uint64_t* d_ooff, const uint64_t* d_caps,
-                          uint64_t* d_sizes, int32_t* d_status)
+                          uint64_t* d_sizes, int32_t* d_status, uint32_t maxN)
 {
-    if (b->codec == PGN_POD5_CODEC_VBZ)
-        return pgn_vbz_compress_batch_device(b->ctx, n, d_samples, d_soff, d_cnt, d_out, d_ooff, d_caps, d_sizes,
-                                             d_status, nullptr, b->stream);
-    return pgn_variant_compress_batch_device(b->ctx, b->codec, n, d_samples, d_soff, d_cnt, d_out, d_ooff, d_caps,
-                                             d_sizes, d_status, nullptr, b->stream);
+    return pgn_compress_batch_bounded(b->ctx, b->codec, maxN ? maxN : 1u, n, d_samples, d_soff, d_cnt, d_out, d_ooff,
+                                      d_caps, d_sizes, d_status, nullptr, b->stream);
 }
 
 static int batch_decompress(pgn_pod5_batch* b, size_t n, const uint8_t* d_in, const uint64_t* d_ioff,
                             const uint64_t* d_isz, int16_t* d_samples, const uint64_t* d_soff, const uint32_t* d_cnt,
-                            int32_t* d_status)
+                            int32_t* d_status, uint32_t maxN)
 {
-    if (b->codec == PGN_POD5_CODEC_VBZ)
-        return pgn_vbz_decompress_batch_device(b->ctx, n, d_in, d_ioff, d_isz, d_samples, d_soff, d_cnt, d_status,
-                                               b->stream);
-    return pgn_variant_decompress_batch_device(b->ctx, b->codec, n, d_in, d_ioff, d_isz, d_samples, d_soff, d_cnt,
-                                               d_status, b->stream);
+    return pgn_decompress_batch_bounded(b->ctx, b->codec, maxN ? maxN : 1u, n, d_in, d_ioff, d_isz, d_samples, d_soff,
+                                        d_cnt, d_status, b->stream);
 }
 
 // every queued transfer and launch of the batch has finished
@@ -504,7 +501,8 @@ int pgn_pod5_compress_reads(pgn_pod5_batch* b, uint32_t read_count, const int16_
         uint8_t* dm = b->dMeta[s].p;
         rc = batch_compress(b, m, (const int16_t*)b->dIn[s].p, (const uint64_t*)(dm + mSoff),
                             (const uint32_t*)(dm + mCnt), b->dOut[s].p, (const uint64_t*)(dm + mOoff),
-                            (const uint64_t*)(dm + mCaps), (uint64_t*)(dm + mSizes), (int32_t*)(dm + mStatus));
+                            (const uint64_t*)(dm + mCaps), (uint64_t*)(dm + mSizes), (int32_t*)(dm + mStatus),
+                            b->chunk);
         if (rc) {
             batch_drain(b);
             return rc;
@@ -602,11 +600,13 @@ int pgn_pod5_decompress_rows(pgn_pod5_batch* b, uint32_t row_count, const uint64
         uint64_t* hIsz = (uint64_t*)(hm + mIsz);
         uint64_t* hSoff = (uint64_t*)(hm + mSoff);
         uint32_t* hCnt = (uint32_t*)(hm + mCnt);
+        uint32_t maxCnt = 0;
         for (size_t i = 0; i < m; i++) {
             hIoff[i] = offsets[r0 + i] - offsets[r0];
             hIsz[i] = offsets[r0 + i + 1] - offsets[r0 + i];
             hSoff[i] = sampleStart[r0 + i] - sampleStart[r0];
             hCnt[i] = samples[r0 + i];
+            maxCnt = samples[r0 + i] > maxCnt ? samples[r0 + i] : maxCnt;
         }
         if (j >= 2) P5CHK(hipStreamWaitEvent(b->copy, b->evComp[s], 0));
         if (bytes) P5CHK(hipMemcpyAsync(b->dIn[s].p, b->hIn[s].p, bytes, hipMemcpyHostToDevice, b->copy));
@@ -617,7 +617,7 @@ int pgn_pod5_decompress_rows(pgn_pod5_batch* b, uint32_t row_count, const uint64
         uint8_t* dm = b->dMeta[s].p;
         rc = batch_decompress(b, m, b->dIn[s].p, (const uint64_t*)(dm + mIoff), (const uint64_t*)(dm + mIsz),
                               (int16_t*)b->dOut[s].p, (const uint64_t*)(dm + mSoff), (const uint32_t*)(dm + mCnt),
-                              (int32_t*)(dm + mStatus));
+                              (int32_t*)(dm + mStatus), maxCnt);
         if (rc) {
             batch_drain(b);
             return rc;
@@ -682,6 +682,8 @@ static int transcode_rows(pgn_ctx* ctx, int srcType, int dst_signal_type, int pg
     dst.codec = dstCodec;
     auto body = [&]() -> int {
         if (n >= (1u << 31)) return PGN_ERR_UNSUPPORTED;
+        uint32_t maxCnt = 0;
+        for (size_t i = 0; i < n; i++) maxCnt = samples[i] > maxCnt ? samples[i] : maxCnt;
         for (size_t i = 0; i < n; i++)
             if (samples[i] > PGN_MAX_CHUNK_SAMPLES) {
                 snprintf(g_pod5_err, sizeof(g_pod5_err), "row %zu: %u samples above PGN_MAX_CHUNK_SAMPLES", i,
@@ -730,7 +732,7 @@ static int transcode_rows(pgn_ctx* ctx, int srcType, int dst_signal_type, int pg
             P5CHK(hipEventRecord(ev[0], stream));
             int r = batch_decompress(&src, n, d + oIn, (const uint64_t*)(d + oIoff), (const uint64_t*)(d + oIsz),
                                      (int16_t*)(d + oSamples), (const uint64_t*)(d + oSoff),
-                                     (const uint32_t*)(d + oCnt), (int32_t*)(d + oStatus));
+                                     (const uint32_t*)(d + oCnt), (int32_t*)(d + oStatus), maxCnt);
             if (r) return r;
             P5CHK(hipEventRecord(ev[1], stream));
             std::vector<int32_t> st(n);
@@ -753,7 +755,7 @@ static int transcode_rows(pgn_ctx* ctx, int srcType, int dst_signal_type, int pg
         P5CHK(hipEventRecord(ev[2], stream));
         int r = batch_compress(&dst, n, (const int16_t*)(d + oSamples), (const uint64_t*)(d + oSoff),
                                (const uint32_t*)(d + oCnt), d + oOut, (const uint64_t*)(d + oOoff),
-                               (const uint64_t*)(d + oCaps), (uint64_t*)(d + oSizes), (int32_t*)(d + oStatus));
+                               (const uint64_t*)(d + oCaps), (uint64_t*)(d + oSizes), (int32_t*)(d + oStatus), maxCnt);
         if (r) return r;
         P5CHK(hipEventRecord(ev[3], stream));
         hipLaunchKernelGGL(pod5_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint64_t*)(d + oSizes),

@@ -132,15 +132,24 @@ __device__ inline uint32_t wave_match_count(const uint8_t* src, uint32_t a, uint
 
 // Hash-table entries, 32 bits: a per-slot epoch tag in the top 5 bits (any other tag reads as an
 // empty slot; the table is cleared once per kTagEpochs - 1 frames), the index (position + 1) in the
-// low idxBits (17 for frames up to 128 KiB, 20 up to kMaxFrameSrc = 512 KiB), and between them a
-// fingerprint of MEM_read32 at the position (10 or 7 bits).  A candidate whose fingerprint differs
+// low idxBits (17 for frames up to 128 KiB, 20 up to 1 MiB, then the frame's bit length up to 26),
+// and between them a fingerprint of MEM_read32 at the position (10 bits down to 1).  A candidate whose fingerprint differs
 // is no match without reading the stream; one whose fingerprint agrees is confirmed by one read of
 // its 4 bytes.  Four bytes per entry keep a slot's table at 2^hashLog x 4 B (32 KiB for the
 // hashLog-13 streams), half of an entry that carries the bytes.
 constexpr uint32_t kTagShift = 27;
 constexpr uint32_t kTagEpochs = 1u << (32 - kTagShift);
-static_assert(z1::kMaxFrameSrc + 2 < (1u << 20), "index field");
-__device__ inline uint32_t ht_idx_bits(uint32_t frameN) { return frameN + 2 < (1u << 17) ? 17u : 20u; }
+// the largest frame source: an index field of 26 bits leaves one fingerprint bit
+constexpr uint32_t kMaxIdxBits = 26;
+constexpr size_t kMaxFrameBytes = ((size_t)1 << kMaxIdxBits) - 2;
+__host__ __device__ inline uint32_t ht_idx_bits(uint32_t frameN)
+{
+    if (frameN + 2 < (1u << 17)) return 17u;
+    if (frameN + 2 < (1u << 20)) return 20u;
+    uint32_t b = 21;
+    while (b < kMaxIdxBits && frameN + 2 >= (1u << b)) b++;
+    return b;
+}
 // the fingerprint field of the entry for these 4 bytes (bits [idxBits, kTagShift))
 __device__ inline uint32_t ht_fp(uint32_t bytes, uint32_t idxBits)
 {
@@ -232,7 +241,8 @@ struct SearchOut {
 };
 __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ src, uint32_t start, uint32_t end, unsigned hlog,
                                                    unsigned mls, uint32_t* __restrict__ ht, uint32_t tag,
-                                                   z1::Seq* __restrict__ seqs, uint32_t rep0, uint32_t rep1, uint32_t idxBits)
+                                                   z1::Seq* __restrict__ seqs, uint32_t rep0, uint32_t rep1, uint32_t idxBits,
+                                                   uint32_t lowIdx, uint32_t maxRep)
 {
     EncLds& L = sEnc;
     const uint32_t lane = (uint32_t)lane_id();
@@ -253,10 +263,14 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     const uint32_t idxMask = (1u << idxBits) - 1u, fpMask = ((1u << kTagShift) - 1u) & ~idxMask;
     const int32_t iend = (int32_t)end, ilimit = (int32_t)end - 8;
     int32_t ip0 = (int32_t)start + (start == 0 ? 1 : 0), anchor = (int32_t)start;
-    // ZSTD_compressBlock_fast_generic: repeat offsets beyond the first position are invalidated
+    // ZSTD_compressBlock_fast_generic: repeat offsets beyond the window at the first position are
+    // invalidated (maxRep); table candidates must lie above the block's lowest prefix index lowIdx
+    // (1 for a frame within its window; ZSTD_getLowestPrefixIndex of the block's end above it)
+    lowIdx = uni(lowIdx);
+    maxRep = uni(maxRep);
     uint32_t off1 = rep0, off2 = rep1, offSaved = 0;
-    if (off2 > (uint32_t)ip0) { offSaved = off2; off2 = 0; }
-    if (off1 > (uint32_t)ip0) { offSaved = off1; off1 = 0; }
+    if (off2 > maxRep) { offSaved = off2; off2 = 0; }
+    if (off1 > maxRep) { offSaved = off1; off1 = 0; }
     uint32_t nbSeq = 0, rounds = 0, candIters = 0;
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
@@ -354,8 +368,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         bool rep = false, c0 = false, c1 = false;
         if (valid) {
             rep = (off1 > 0) && (repw == (uint32_t)(v8 >> 16));
-            c0 = (m0 > 1) && (fw0 ? d0 == (uint32_t)v8 : fpok0);
-            c1 = (m1 > 1) && (fw1 ? d1 == (uint32_t)(v8 >> 8) : fpok1);
+            c0 = (m0 > lowIdx) && (fw0 ? d0 == (uint32_t)v8 : fpok0);
+            c1 = (m1 > lowIdx) && (fw1 ? d1 == (uint32_t)(v8 >> 8) : fpok1);
         }
 #ifdef PGN_PROFILE
         candIters += wave_max(myIt);
@@ -443,7 +457,8 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
             off1 = (uint32_t)(ipm - match0);
             offcode = off1 + 2;
             mLength = 4;
-            const int32_t lim = (ipm - anchor) < match0 ? (ipm - anchor) : match0;
+            const int32_t room = match0 - ((int32_t)lowIdx - 1);  // down to the window's first position
+            const int32_t lim = (ipm - anchor) < room ? (ipm - anchor) : room;
             const uint32_t back = lim > 0 ? wave_back_count(src, (uint32_t)ipm, (uint32_t)match0, (uint32_t)lim) : 0u;
             ipm -= (int32_t)back;
             match0 -= (int32_t)back;
@@ -1646,14 +1661,14 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         if (lane == 0) z1::write_empty_frame(dst);
         return 9;
     }
-    const size_t h = z1::frame_header_size(n);
+    const size_t h = z1::frame_header_size(n, n < 7 ? 10u : z1::level1_params(n).windowLog);
     if (n < 7) {
         if (lane == 0) z1::write_raw_block_frame(dst, src, n);
         return h + 3 + n;
     }
     const z1::Params p = z1::level1_params(n);
     P.count(12);
-    if (lane == 0) z1::write_frame_header(dst, n);
+    if (lane == 0) z1::write_frame_header(dst, n, p.windowLog);
     size_t o = h;
     uint32_t rep0 = 1, rep1 = 4;  // confirmed repeat offsets (rep[2] is never read at level 1)
     uint32_t hufCur = 0, hufCheck = 0;
@@ -1668,8 +1683,10 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
 #else
         if (bs >= 7) {
 #endif
+            const uint32_t ip0 = start + (start == 0 ? 1u : 0u);
             const SearchOut so = fast_search_wave(src, start, start + bs, p.hashLog, p.mls, S.ht, tag, S.seqs, rep0, rep1,
-                                                      ht_idx_bits(n));
+                                                  ht_idx_bits(n), z1::window_low_index(start + bs, p.windowLog),
+                                                  ip0 + 1u - z1::window_low_index(ip0, p.windowLog));
             const uint32_t nbSeq = uni(so.nbSeq), lastLL = uni(so.lastLL);
             P.mark(1);
             P.count(0, uni(so.rounds));

@@ -113,7 +113,7 @@ PGN_HD unsigned ml_code(uint32_t mlBase)
 // Level-1 compression parameters: row `level 1` of the four srcSize tiers of
 // ZSTD_defaultCParameters, then ZSTD_adjustCParams_internal (window shrunk to the source,
 // hashLog <= windowLog + 1, windowLog >= 10); equal to libzstd 1.4.8/1.4.9's
-// ZSTD_getCParams(1, srcSize, 0) for every size up to kMaxFrameSrc (tests/test_zstd_model.py).
+// ZSTD_getCParams(1, srcSize, 0) for every size (tests/test_zstd_model.py).
 // ---------------------------------------------------------------------------------------------
 struct Params {
     unsigned windowLog, hashLog, mls;
@@ -159,23 +159,34 @@ PGN_HD uint32_t hash_word(uint64_t v, unsigned hlog, unsigned mls)
 PGN_HD uint32_t hash_at(const uint8_t* p, unsigned hlog, unsigned mls) { return hash_word(rd64(p), hlog, mls); }
 
 // ---------------------------------------------------------------------------------------------
-// Frame header (ZSTD_writeFrameHeader, single segment, content size present, no checksum/dictID)
+// Frame header (ZSTD_writeFrameHeader: content size present, no checksum / dictID; single segment
+// when the window covers the source, else a window descriptor byte (windowLog - 10) << 3)
 // ---------------------------------------------------------------------------------------------
-PGN_HD size_t write_frame_header(uint8_t* op, size_t srcSize)
+PGN_HD size_t write_frame_header(uint8_t* op, size_t srcSize, unsigned windowLog)
 {
     wr32(op, kMagic);
+    const unsigned single = ((size_t)1 << windowLog) >= srcSize;
     unsigned fcsCode = (srcSize >= 256) + (srcSize >= 65536 + 256) + (srcSize >= 0xFFFFFFFFull);
-    op[4] = (uint8_t)((1u << 5) + (fcsCode << 6));
+    op[4] = (uint8_t)((single << 5) + (fcsCode << 6));
+    size_t pos = 5;
+    if (!single) op[pos++] = (uint8_t)((windowLog - 10u) << 3);
     switch (fcsCode) {
-    case 0: op[5] = (uint8_t)srcSize; return 6;
-    case 1: wr16(op + 5, (uint32_t)(srcSize - 256)); return 7;
-    default: wr32(op + 5, (uint32_t)srcSize); return 9;
+    case 0: op[pos] = (uint8_t)srcSize; return pos + 1;
+    case 1: wr16(op + pos, (uint32_t)(srcSize - 256)); return pos + 2;
+    default: wr32(op + pos, (uint32_t)srcSize); return pos + 4;
     }
 }
-PGN_HD size_t frame_header_size(size_t srcSize)
+PGN_HD size_t frame_header_size(size_t srcSize, unsigned windowLog)
 {
     unsigned fcsCode = (srcSize >= 256) + (srcSize >= 65536 + 256);
-    return fcsCode == 0 ? 6 : (fcsCode == 1 ? 7 : 9);
+    return (fcsCode == 0 ? 6 : (fcsCode == 1 ? 7 : 9)) + (((size_t)1 << windowLog) < srcSize);
+}
+// ZSTD_getLowestPrefixIndex(ms, end index, windowLog) of a frame (dictLimit 1, no dictionary): the
+// lowest index a match candidate of a block ending at position `end` may exceed.
+PGN_HD uint32_t window_low_index(size_t end, unsigned windowLog)
+{
+    const size_t maxDist = (size_t)1 << windowLog;
+    return end > maxDist ? (uint32_t)(end + 1 - maxDist) : 1u;
 }
 
 // Literal section headers (ZSTD_noCompressLiterals / ZSTD_compressRleLiteralsBlock).

@@ -1,5 +1,5 @@
 // zstd1_model.h -- serial composition of zstd1_common.h into a full `ZSTD_compress(.., 1)` for one
-// source of at most kMaxFrameSrc (512 KiB: a single-segment frame of up to four 128 KiB blocks).
+// source (a single-segment frame up to 512 KiB, a window-descriptor frame above).
 //
 // Host and device: the GPU kernels run the serial parts of these on one lane; the host build
 // (libpgn_model.so, test-only) lets the test-suite fuzz the exact same code against libzstd.
@@ -14,9 +14,10 @@ namespace z1 {
 
 // ---------------------------------------------------------------------------------------------
 // ZSTD_compressBlock_fast (libzstd 1.4.x, two positions per step, kSearchStrength 8, stepSize 2) over
-// the block [start, end) of a source whose window is the whole source (single segment): window base
-// = src - 1 (prefixStartIndex 1), table entries hold indices (= offset + 1) and persist across the
-// blocks of a frame (the caller zeroes the table once per frame).  rep[0..1] are the confirmed
+// the block [start, end) of a frame: window base = src - 1 (table entries hold indices = offset + 1,
+// and persist across the blocks of a frame; the caller zeroes the table once per frame).  A source
+// within the window (single segment, n <= 2^windowLog) has prefixStartIndex 1; above it, the block's
+// candidates must lie within 2^windowLog of the block's end (ZSTD_getLowestPrefixIndex).  rep[0..1] are the confirmed
 // repeat offsets on entry and the block's candidates on exit (ZSTD_compressBlock_fast_generic's
 // offsetSaved rule); at the first position of the frame, offset_2 (4) > maxRep (1) is invalidated.
 // Appends sequences (literal runs are implied: src[anchor .. anchor + litLength)); returns nbSeq,
@@ -37,9 +38,13 @@ PGN_HD size_t fast_search_serial(const uint8_t* src, size_t start, size_t end, c
     long ip0 = (long)start + (start == 0 ? 1 : 0), anchor = (long)start;
     long ip1 = ip0 + 1;
     const long iend = (long)end, ilimit = (long)end - 8;
+    // ZSTD_getLowestPrefixIndex: candidates must lie within the window of the block's end
+    const uint32_t lowIdx = window_low_index(end, p.windowLog);
+    const long prefixStart = (long)lowIdx - 1;  // its position
     uint32_t offset_1 = rep[0], offset_2 = rep[1], offsetSaved = 0;
     {
-        const uint32_t maxRep = (uint32_t)ip0;  // current - windowLow = (ip0 + 1) - 1
+        // current - windowLow at the first position
+        const uint32_t maxRep = (uint32_t)ip0 + 1u - window_low_index((size_t)ip0, p.windowLog);
         if (offset_2 > maxRep) { offsetSaved = offset_2; offset_2 = 0; }
         if (offset_1 > maxRep) { offsetSaved = offset_1; offset_1 = 0; }
     }
@@ -63,10 +68,10 @@ PGN_HD size_t fast_search_serial(const uint8_t* src, size_t start, size_t end, c
             offcode = 0;
         } else {
             bool found = false;
-            if ((mi0 > 1) && rd32(src + mi0 - 1) == val0) {
+            if ((mi0 > lowIdx) && rd32(src + mi0 - 1) == val0) {
                 match0 = (long)mi0 - 1;
                 found = true;
-            } else if ((mi1 > 1) && rd32(src + mi1 - 1) == val1) {
+            } else if ((mi1 > lowIdx) && rd32(src + mi1 - 1) == val1) {
                 ip0 = ip1;
                 match0 = (long)mi1 - 1;
                 found = true;
@@ -81,7 +86,7 @@ PGN_HD size_t fast_search_serial(const uint8_t* src, size_t start, size_t end, c
             offset_1 = (uint32_t)(ip0 - match0);
             offcode = offset_1 + 2;
             mLength = 4;
-            while ((ip0 > anchor) && (match0 > 0) && (src[ip0 - 1] == src[match0 - 1])) {
+            while ((ip0 > anchor) && (match0 > prefixStart) && (src[ip0 - 1] == src[match0 - 1])) {
                 ip0--;
                 match0--;
                 mLength++;
@@ -361,13 +366,13 @@ PGN_HD size_t compress_sequences(uint8_t* dst, const Seq* seqs, size_t nbSeq, ui
 // ---------------------------------------------------------------------------------------------
 PGN_HD size_t write_empty_frame(uint8_t* dst)
 {
-    size_t h = write_frame_header(dst, 0);
+    size_t h = write_frame_header(dst, 0, 10);
     wr24(dst + h, 1u + (kBtRaw << 1));
     return h + 3;
 }
 PGN_HD size_t write_raw_block_frame(uint8_t* dst, const uint8_t* src, size_t n)
 {
-    size_t h = write_frame_header(dst, n);
+    size_t h = write_frame_header(dst, n, 10);
     wr24(dst + h, (uint32_t)(1u + (kBtRaw << 1) + (n << 3)));
     for (size_t i = 0; i < n; i++) dst[h + 3 + i] = src[i];
     return h + 3 + n;
@@ -441,7 +446,8 @@ PGN_HD size_t compress_block(uint8_t* dst, const uint8_t* src, size_t start, siz
     return 3 + cSize;
 }
 
-// Full serial ZSTD_compress(dst, bound, src, n, 1) for n <= kMaxFrameSrc (blocks of 128 KiB).
+// Full serial ZSTD_compress(dst, bound, src, n, 1) (blocks of 128 KiB; a window-descriptor frame
+// above 2^windowLog = 512 KiB).
 // `ht`: 2^15 entries; `seqs`, `llC/ofC/mlC`: kMaxSrc/4 + 2 entries; `litbuf`: kMaxSrc bytes
 // (per block); dst capacity >= compress_bound(n).
 PGN_HD size_t compress_serial(uint8_t* dst, const uint8_t* src, size_t n, uint32_t* ht, Seq* seqs, uint8_t* llC,
@@ -454,7 +460,7 @@ PGN_HD size_t compress_serial(uint8_t* dst, const uint8_t* src, size_t n, uint32
     uint32_t rep[3] = {1, 4, 8};
     w.huf[0].check = false;
     for (int s = 0; s < 256; s++) { w.huf[0].nbBits[s] = 0; w.huf[0].val[s] = 0; }
-    size_t o = write_frame_header(dst, n);
+    size_t o = write_frame_header(dst, n, p.windowLog);
     for (size_t start = 0; start < n; start += kMaxSrc) {
         const size_t bs = (n - start < kMaxSrc) ? n - start : kMaxSrc;
         o += compress_block(dst + o, src, start, bs, start + bs == n, start == 0, p, ht, rep, seqs, llC, ofC, mlC, litbuf, w);

@@ -1,8 +1,9 @@
-"""GPU parity of multi-block zstd frames (streams above one 128 KiB block, up to 512 KiB): chunks of
-up to PGN_MAX_CHUNK_SAMPLES (262,144) samples for C5, and noisy VBZ / C1 chunks whose svb16 buffer
-exceeds one block (the reference's ZSTD_compress takes any size: signal_compression.cpp:57-66,
-C5.hpp:337-413).  Frames equal libzstd 1.4.x's byte for byte (through the oracle) and round-trip,
-per chunk and batched.  Needs an MI355X."""
+"""GPU parity of multi-block zstd frames (streams above one 128 KiB block): C5 chunks up to and above
+the batched passes' 262,144 samples (the large-chunk pass, up to PGN_MAX_CHUNK_SAMPLES), noisy VBZ /
+C1 chunks whose svb16 buffer exceeds one block, and frames above 512 KiB (windowLog 19 < source:
+window-descriptor frames whose matches stay inside the window).  The reference's ZSTD_compress
+takes any size (signal_compression.cpp:57-66, C5.hpp:337-413).  Frames equal libzstd 1.4.x's byte
+for byte (through the oracle) and round-trip, per chunk and batched.  Needs an MI355X."""
 import numpy as np
 import pytest
 
@@ -37,20 +38,48 @@ def test_c5_large_chunks_identical(codec):
 
 
 def test_c5_over_limit_is_unsupported(codec):
-    from rawnanoporesignalcompression_amd import PGNanoError
+    from rawnanoporesignalcompression_amd import PGN_MAX_CHUNK_SAMPLES, PGNanoError
 
-    x = O.synth_read(1, MAX + 1)
+    x = np.zeros(PGN_MAX_CHUNK_SAMPLES + 1, np.int16)
     with pytest.raises(PGNanoError) as ei:
         codec.compress_signal(x)
     assert ei.value.status == 9
 
 
-def test_c5_batch_mixed_sizes(codec):
+BIG = [MAX + 1, 300000, 600000, 1048576]
+
+
+@pytest.mark.parametrize("n", BIG)
+def test_c5_chunks_above_batched_pass(codec, n):
+    """Chunks above 262,144 samples (the large-chunk pass); from 524,289 samples the M/L streams
+    are frames above 512 KiB (window descriptor, windowed matches)."""
+    for x in (O.synth_read(9000 + n, n), _noisy(n, n, 25)):
+        rc, ref, _ = O.c5_compress(x)
+        assert rc == 0
+        assert codec.compress_signal(x) == ref, n
+        assert np.array_equal(codec.decompress_signal(ref, sample_count=x.size), x), n
+
+
+def test_c5_long_range_repeats_outside_window(codec):
+    """A stream whose repeats lie 600,000 bytes back (beyond the 512 KiB window) and 400,000 bytes
+    back (inside it): libzstd matches only the latter."""
+    base = _noisy(400000, 31, 30)
+    x = np.concatenate([base, _noisy(200000, 32, 30), base[:300000], base[100000:400000]])
+    rc, ref, _ = O.c5_compress(x)
+    assert rc == 0
+    assert codec.compress_signal(x) == ref
+    assert np.array_equal(codec.decompress_signal(ref, sample_count=x.size), x)
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_c5_batch_mixed_sizes(codec, big):
     import torch
 
     rng = np.random.default_rng(21)
     counts = rng.integers(100000, MAX + 1, 96).astype(np.int32)
     counts[:4] = [131072, 131073, MAX, 7]
+    if big:  # chunks for the large-chunk pass among the batched ones (the last call's buffers are reused)
+        counts[[5, 17, 40, 41, 95]] = [MAX + 1, 1048576, 700000, 300001, 2000000]
     samples, offs, cnt = codec.synth_reads(len(counts), counts, seed=42)
     enc = codec.compress_batch(samples, offs, cnt)
     out, _, st = codec.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
@@ -59,7 +88,7 @@ def test_c5_batch_mixed_sizes(codec):
     assert torch.equal(out, samples)
     blobs = enc.blobs.cpu().numpy()
     bo, bs = enc.offsets.cpu().numpy(), enc.sizes.cpu().numpy()
-    for r in list(range(0, len(counts), 7)) + [1, 2]:
+    for r in list(range(0, len(counts), 7)) + [1, 2] + ([5, 17, 40, 41, 95] if big else []):
         rc, ref, _ = O.c5_compress(O.synth_read(r, int(counts[r])))
         assert rc == 0 and blobs[bo[r]:bo[r] + bs[r]].tobytes() == ref, (r, int(counts[r]))
 
@@ -98,19 +127,36 @@ def test_vbz_noisy_default_chunk(vbz):
         assert blobs[bo[i]:bo[i] + bs[i]].tobytes() == O.vbz_compress(x), i
 
 
-def test_vbz_limits(vbz):
-    """svb16 up to 512 KiB is encoded (four blocks); above it the chunk is reported unsupported."""
-    from rawnanoporesignalcompression_amd import PGNanoError
-
-    x = np.random.default_rng(8).integers(-32768, 32768, 240000).astype(np.int16)  # svb16 ~ 510,000 B
+@pytest.mark.parametrize("n", [240000, MAX, 400000, 1000000])
+def test_vbz_svb16_above_512k(vbz, n):
+    """Uniform noise: svb16 buffers of ~2.1 n bytes -- 510,000 B (four blocks, single segment) up to
+    2.1 MB (window-descriptor frames, above the batched pass from 262,145 samples)."""
+    x = np.random.default_rng(n).integers(-32768, 32768, n).astype(np.int16)
     ref = O.vbz_compress(x)
     assert vbz.compress_signal(x) == ref
     assert np.array_equal(vbz.decompress_signal(ref, sample_count=x.size), x)
-    y = np.random.default_rng(9).integers(-32768, 32768, MAX).astype(np.int16)  # svb16 ~ 557,000 B
-    with pytest.raises(PGNanoError) as ei:
-        vbz.compress_signal(y)
-    assert ei.value.status == 9
-    assert np.array_equal(vbz.decompress_signal(O.vbz_compress(y), sample_count=y.size), y)
+
+
+def test_vbz_batch_with_large_chunks(vbz):
+    import torch
+
+    rng = np.random.default_rng(77)
+    xs = [rng.integers(-32768, 32768, n).astype(np.int16) for n in (102400, 400000, 5000, MAX + 10)]
+    xs.append(_noisy(1200000, 78, 400))
+    flat = np.concatenate(xs)
+    dev = torch.device("cuda", 0)
+    counts_np = np.array([x.size for x in xs], np.int64)
+    samples = torch.from_numpy(flat).to(dev)
+    counts = torch.from_numpy(counts_np.astype(np.int32)).to(dev)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(counts_np)[:-1]])).to(dev)
+    enc = vbz.compress_batch(samples, offs, counts)
+    out, _, st = vbz.decompress_batch(enc.blobs, enc.offsets, enc.sizes, counts)
+    torch.cuda.synchronize()
+    assert (enc.status == 0).all() and (st == 0).all() and torch.equal(out, samples)
+    blobs = enc.blobs.cpu().numpy()
+    bo, bs = enc.offsets.cpu().numpy(), enc.sizes.cpu().numpy()
+    for i, x in enumerate(xs):
+        assert blobs[bo[i]:bo[i] + bs[i]].tobytes() == O.vbz_compress(x), i
 
 
 def test_c1_large_data_frame():
@@ -118,7 +164,7 @@ def test_c1_large_data_frame():
 
     c = PGNanoCodec(0, variant="C1")
     try:
-        for i, x in enumerate([_noisy(102400, 10, 3000), O.synth_read(11, 200000)]):
+        for i, x in enumerate([_noisy(102400, 10, 3000), O.synth_read(11, 200000), _noisy(400000, 12, 3000)]):
             rc, ref, _ = O.variant_compress("C1", x)
             assert rc == O.OK
             assert c.compress_signal(x) == ref, i

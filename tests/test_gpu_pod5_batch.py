@@ -63,7 +63,7 @@ def test_reference_signal_column_reproduced():
         vz.close()
 
 
-@pytest.mark.parametrize("chunk", [0, 65536, 262144])
+@pytest.mark.parametrize("chunk", [0, 65536, 262144, 1048576])
 def test_pgnano_batch_matches_per_chunk_oracle(codec, chunk):
     from rawnanoporesignalcompression_amd import Pod5SignalBatch
 

@@ -176,3 +176,25 @@ def test_multiblock_fuzz_bounded():
         assert model_compress(b) == ref, (n, kind, cnt)
         cnt += 1
     assert cnt > 20
+
+
+# ---- frames above 512 KiB: windowLog 19 < source (window descriptor, matches inside the window) ----
+BIG_SIZES = [524289, 600000, 1048576, 1500001]
+
+
+@pytest.mark.parametrize("n", BIG_SIZES)
+def test_window_descriptor_frames(n):
+    """The model (the code the GPU encoder shares) equals libzstd 1.4.x above one single-segment
+    frame: ZSTD_getLowestPrefixIndex bounds the candidates of each block by the window of its end."""
+    rng = np.random.default_rng(n)
+    for kind in (1, 3, 7, 10):
+        b = np.ascontiguousarray(gen_multiblock(rng, n, kind), dtype=np.uint8)
+        if kind == 7:  # copies 400,000 (inside the window) and 700,000 (outside) bytes back
+            for d in (700000, 400000):
+                if n > d + 1000:
+                    b[d:] = np.resize(b[:n - d], n - d)
+        ref = O.zstd_compress1(b)
+        assert ref[4] & 0x20 == 0  # no single-segment flag: a window descriptor
+        assert model_compress(b) == ref, (n, kind)
+        r, d2 = model_decompress(ref, b.size)
+        assert r == b.size and d2 == b.tobytes(), (n, kind)
