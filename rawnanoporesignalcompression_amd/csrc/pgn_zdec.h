@@ -675,7 +675,7 @@ __device__ __forceinline__ uint32_t seqbits_read(SeqBits& b, uint32_t nb)
 // One block's sequences: decode + execute.  Returns the new output position or a negative DecErr.
 __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t seqSize, const uint8_t* lit, size_t rs,
                                                  uint8_t* dst, size_t op, size_t dstCap, size_t frameStart,
-                                                 DecScratch S, bool lastBlock, SeqState& fs)
+                                                 DecScratch S, bool lastBlock, SeqState& fs, PhaseProf& P)
 {
     const int lane = lane_id();
     seqSrc = uni(seqSrc);
@@ -759,6 +759,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
             }
             fs.saved = 7u;
         }
+        P.mark(9);
         // bitstream
         SeqBits br;
         br.bs = seqSrc + pos;
@@ -774,6 +775,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
         uint32_t sOF = seqbits_read(br, tlog[1]);
         uint32_t sML = seqbits_read(br, tlog[2]);
         size_t litPos = 0;
+        P.mark(10);
         for (uint32_t b0 = 0; b0 < nbSeq; b0 += 64) {
             const uint32_t nb = (nbSeq - b0) < 64u ? nbSeq - b0 : 64u;
             // decode a batch
@@ -814,6 +816,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
                 }
             }
             lds_sync();
+            P.mark(13);
             // execute the batch
             for (uint32_t t = 0; t < nb; t++) {
                 const uint32_t ll = sDec.qsq[t][0], ml = sDec.qsq[t][1], off = sDec.qsq[t][2];
@@ -838,6 +841,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
                 op += ml;
                 lds_sync();
             }
+            P.mark(14);
         }
         if (br.pos != 0) return z1::kDecErrCorrupt;
         const size_t remLit = rs - litPos;
@@ -845,6 +849,7 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
         wave_copy(dst + op, lit + litPos, remLit);
         op += remLit;
         lds_sync();
+        P.mark(15);
         fs.rep0 = rep0;
         fs.rep1 = rep1;
         fs.rep2 = rep2;
@@ -876,6 +881,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     S.seg = uni(S.seg);
     S.segCap = uni(S.segCap);
     S.segDiag = uni(S.segDiag);
+    P.mark(3);  // the work unit's fetch (queue, unit record) up to here
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
     HdrWin hw;
@@ -1037,7 +1043,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                     }
                     hufInLds = false;
                     wave_sync();
-                    const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, last != 0, fs);
+                    const long r = exec_sequences_wave(seqSrc, seqSize, lit, rs, dst, op, dstCap, frameStart, S, last != 0, fs, P);
                     P.count(11);
                     if (r < 0) return r;
                     op = (size_t)r;

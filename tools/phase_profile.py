@@ -13,8 +13,9 @@ from rawnanoporesignalcompression_amd import PGNanoCodec
 ENC = ["split", "search", "lit_gather", "hist", "sort", "hdr(writeCTable)", "huf_encode", "raw_lit", "seq",
        "frame_finish", "assemble", "tree_merge", "tree_depth", "tree_maxheight", "tree_canon"]
 TWO = os.environ.get("PGN_HUF") != "seg"
-DEC = ["parse/merge_wait", "huf_table", "huf_copy(ph3)", "seq_list", "seq_exec", "raw_copy", "merge",
-       "lit_hdr", "huf_store(passB)"] + (["-", "-", "huf_spec(passA)", "huf_sync", "-", "-", "-"] if TWO else
+DEC = ["parse/merge_wait", "huf_table", "huf_copy(ph3)", "unit_fetch", "seq_exec(rest)", "raw_copy", "merge",
+       "lit_hdr", "huf_store(passB)"] + (["seq_tables", "seq_bits", "huf_spec(passA)", "huf_sync", "seq_decode",
+                                          "seq_copy", "seq_tail"] if TWO else
                                          ["seg_sync+walk", "seg_compact", "seg_stage", "seg_singles", "seg_bodies",
                                           "seg_tail", "seg_epochs"])
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
