@@ -67,7 +67,7 @@ def parse(argv=None):
     p.add_argument("--no-side", action="store_true",
                    help="skip the STREAM-copy, PCIe-inclusive and per-chunk side measurements (profiling runs: "
                         "the kernel statistics then hold only the bench batch's launches)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     # the other BASELINE configs; the default run is configs[1]
     p.add_argument("--pore", choices=sorted(PORES), default="default",
                    help="generator parameters: dwell per pore chemistry (configs[2] uses r1041)")

@@ -30,18 +30,25 @@ typedef enum pgn_status {
     PGN_ERR_REMAINING = 4,        /* "Remaining data at end of signal buffer"       C5.hpp:675-677 */
     PGN_ERR_ZSTD_COMPRESS = 5,    /* "Failed to compress ..."                        C5.hpp:340-342 */
     PGN_ERR_CORRUPT = 6,          /* input on which the reference reads out of bounds (UB there) */
-    PGN_ERR_UNSUPPORTED = 9,      /* chunk larger than PGN_MAX_CHUNK_SAMPLES, or a stream above 512 KiB */
+    PGN_ERR_UNSUPPORTED = 9,      /* chunk above PGN_MAX_CHUNK_SAMPLES; decode: frames claiming more than 5 bytes
+                                     per sample of the chunk (the intermediate's capacity) */
     PGN_ERR_INVALID_ARG = 10,
     PGN_ERR_HIP = 11,             /* HIP runtime failure (message in pgn_last_error) */
     PGN_ERR_NO_DEVICE = 12,
     PGN_ERR_IO = 13               /* file open/read/write failure (pgnano_pod5file.h) */
 } pgn_status;
 
-/* Largest chunk the GPU path encodes and decodes.  Every stream is one zstd frame of up to four
- * 128 KiB blocks (ZSTD_compress level 1 as libzstd 1.4.x writes it for sources up to 512 KiB); a VBZ
- * or C1 svb16 buffer above 512 KiB (noisy chunks near this limit) is PGN_ERR_UNSUPPORTED.  The
- * reference writer's default chunk is 102,400 samples (pod5/c++/pod5_format/file_writer.h:22) and
- * the chunk size is a writer option (c_api.h:526-539). */
+/* Largest chunk the GPU path encodes and decodes (16 Mi samples; the reference takes any size: its
+ * ZSTD_compress and svb16 calls are unbounded, signal_compression.cpp:57-66, C5.hpp:337-413).  Every
+ * stream is one zstd frame in 128 KiB blocks as libzstd 1.4.x writes it at level 1: single-segment
+ * up to 512 KiB, a window-descriptor frame (windowLog 19, matches within the window) above.  The
+ * reference writer's default chunk is 102,400 samples (pod5/c++/pod5_format/file_writer.h:22); the
+ * chunk size is a writer option (c_api.h:526-539).
+ * Chunks up to 262,144 samples run in the batched passes; larger ones in a second pass of the same
+ * call whose per-chunk buffers are spaced for the largest of them (see the batch calls below).
+ * Decode: a chunk's decoded frames share an intermediate buffer of 5 bytes per sample of the chunk
+ * (a C5 chunk's streams take at most 3.75, an svb16 buffer 2.13 + 16 bytes); a blob whose frames
+ * claim more content is PGN_ERR_UNSUPPORTED. */
 #define PGN_MAX_CHUNK_SAMPLES 16777216u
 
 /* Per-chunk statistics, the reference's global byte counters (src/c++/copy.cpp:64-85, updated at
@@ -95,7 +102,11 @@ int pgn_pod5_vbz_decompress_signal(const char *compressed_signal, size_t compres
 /* Batched, device-resident encode of `nchunks` independent chunks (each <= PGN_MAX_CHUNK_SAMPLES):
  * chunk i = d_samples[d_sample_offsets[i] .. + d_sample_counts[i]) -> d_out[d_out_offsets[i] ..),
  * capacity d_out_caps[i]; d_out_sizes[i] and d_status[i] receive the result.  d_stats (optional)
- * receives PGN_STATS_PER_CHUNK uint64 per chunk. */
+ * receives PGN_STATS_PER_CHUNK uint64 per chunk.
+ * The batch calls are asynchronous on `stream` except for one host wait: the chunks above 262,144
+ * samples are listed by a small kernel that runs after the work queued before the call (while the
+ * batched pass runs) and the host reads their count before queueing their pass.  The wait ends when
+ * the earlier work and that kernel have finished, not the call's own kernels. */
 int pgn_compress_batch_device(pgn_ctx *ctx, size_t nchunks, const int16_t *d_samples,
                               const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts, uint8_t *d_out,
                               const uint64_t *d_out_offsets, const uint64_t *d_out_caps, uint64_t *d_out_sizes,
@@ -114,7 +125,7 @@ size_t pgn_vbz_compressed_signal_max_size(size_t sample_count);
 
 /* pod5::compress_signal(samples, pool, destination) (signal_compression.cpp:21-50): the compressed
  * size in *out_size; a frame larger than dst_capacity is PGN_ERR_ZSTD_COMPRESS ("Failed to compress
- * data").  Chunks whose svb16 buffer exceeds 512 KiB return PGN_ERR_UNSUPPORTED. */
+ * data"). */
 int pgn_vbz_compress_signal(pgn_ctx *ctx, const int16_t *samples, size_t sample_count, uint8_t *dst,
                             size_t dst_capacity, size_t *out_size);
 
@@ -144,8 +155,7 @@ int pgn_vbz_decompress_batch_device(pgn_ctx *ctx, size_t nchunks, const uint8_t 
  *   VBZ0 compress_signal_VBZ1   (VBZ_0.hpp:316-423)              1 frame: 2-bit keys + nibble stream
  * VBZ0 compresses straight into the destination ("Failed to compress data" = PGN_ERR_ZSTD_COMPRESS
  * when the frame does not fit); C1/C2/C3 copy into it unchecked in the reference, here a
- * too-small destination is PGN_ERR_DST_TOO_SMALL with the required size, as for C5/C4.  Streams
- * above 512 KiB return PGN_ERR_UNSUPPORTED. */
+ * too-small destination is PGN_ERR_DST_TOO_SMALL with the required size, as for C5/C4. */
 typedef enum pgn_variant {
     PGN_VARIANT_C5 = 0,
     PGN_VARIANT_C4 = 1,

@@ -1628,7 +1628,7 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
 }
 
 // ---------------------------------------------------------------------------------------------
-// One stream -> one frame of up to kMaxFrameSrc bytes (ZSTD_compress_frameChunk: blocks of 128 KiB;
+// One stream -> one frame of up to kMaxFrameBytes (ZSTD_compress_frameChunk: blocks of 128 KiB;
 // the block logic and the state a frame carries across its blocks -- hash table, repeat offsets,
 // Huffman table -- are zstd1_model.h compress_block).  dst must have compress_bound(n) bytes.
 // Returns the frame size.

@@ -31,7 +31,6 @@ constexpr unsigned kLLFSELog = 9, kMLFSELog = 9, kOffFSELog = 8;
 constexpr unsigned kMaxLL = 35, kMaxML = 52, kMaxOff = 31, kDefaultMaxOff = 28;
 constexpr unsigned kLLDefaultNormLog = 6, kMLDefaultNormLog = 6, kOFDefaultNormLog = 5;
 constexpr size_t kMaxSrc = 131072;        // ZSTD_BLOCKSIZE_MAX: one block (literals, sequences per block)
-constexpr size_t kMaxFrameSrc = 524288;  // largest stream encoded here: a single-segment frame (windowLog 19)
 
 enum : unsigned { kSetBasic = 0, kSetRle = 1, kSetCompressed = 2, kSetRepeat = 3 };
 enum : unsigned { kBtRaw = 0, kBtRle = 1, kBtCompressed = 2 };
