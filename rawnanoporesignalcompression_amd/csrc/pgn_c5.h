@@ -405,17 +405,21 @@ struct MergePlan {
     uint32_t nbS, nbM;
 };
 
+// The merge of the steps [t0, t1) of a chunk (t0 a multiple of kSplitStep, t1 = n or one), given
+// the class counts of the samples before t0 (sN0 / mN0 / lN0) and the running sum there (carry, in
+// and out); *lEnd receives the class-3 count through t1.  c5_merge_wave is the whole chunk in one
+// call; dec_merge_wg_kernel gives the ranges of one chunk to the waves of a workgroup.
 template <bool C4 = false>
-__device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
-                                             uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint64_t* consumed,
-                                             MergeLds& W)
+__device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
+                                              uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint32_t t0,
+                                              uint32_t t1, uint64_t sN0, uint64_t mN0, uint64_t lN0, uint32_t& carry,
+                                              uint64_t* lEnd, MergeLds& W)
 {
     using CO = ClassOffsets<C4>;
     const uint32_t lane = (uint32_t)lane_id();
     const uint64_t kl = ((uint64_t)n + 3) / 4;
     const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
-    uint64_t sN = 0, mN = 0, lN = 0;  // nibbles / bytes consumed so far (wave-uniform)
-    uint32_t carry = 0;
+    uint64_t sN = sN0, mN = mN0, lN = lN0;  // nibbles / bytes consumed so far (wave-uniform)
     if (lane == 0) W.zero[0] = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {  // the S table: byte -> two entries
@@ -467,14 +471,14 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
         pn.nbM = (uint32_t)((pn.aM + pn.nm - pn.aM0 + 15) >> 4);
         return true;
     };
-    if (n == 0) {
-        *consumed = ph;
+    if (t0 >= t1) {
+        *lEnd = lN;
         return 0;
     }
-    // prologue: step 0's plan and staged bytes, step 1's key word
+    // prologue: step t0's plan and staged bytes, step t0 + 1's key word
     MergePlan cur;
-    if (!plan(0, key_word(0), cur)) return 1;
-    uint32_t kwNext = kSplitStep < n ? key_word(kSplitStep) : 0u;
+    if (!plan(t0, key_word(t0), cur)) return 1;
+    uint32_t kwNext = t0 + kSplitStep < t1 ? key_word(t0 + kSplitStep) : 0u;
     uint4 vS = make_uint4(0, 0, 0, 0), vM = vS;
     uint32_t lb = 0, hb = 0;
     auto load_stage = [&](const MergePlan& pn) {
@@ -487,7 +491,7 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
     };
     load_stage(cur);
     lds_sync();
-    for (uint32_t t = 0; t < n; t += kSplitStep) {
+    for (uint32_t t = t0; t < t1; t += kSplitStep) {
         const bool full = t + kSplitStep <= n;
         // ---- this step's bytes into the window (loaded a step ago): S by table, M and class 3 by arithmetic
         const uint32_t eM = 32u * cur.nbS, eL = eM + 16u * cur.nbM;
@@ -525,17 +529,101 @@ __device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uin
         lN += cur.nl;
         // ---- the next step: its plan (key word loaded a step ago), its bytes in flight during this merge
         const uint32_t tn = t + kSplitStep;
-        bool more = tn < n;
+        bool more = tn < t1;
         if (more) {
             if (!plan(tn, kwNext, cur)) return 1;
-            if (tn + kSplitStep < n) kwNext = key_word(tn + kSplitStep);
+            if (tn + kSplitStep < t1) kwNext = key_word(tn + kSplitStep);
             load_stage(cur);
         }
         merge_step(W, kw, pS, pM, pL, carry, out, t, n, full);
         lds_sync();
     }
-    *consumed = ph + lN;
+    *lEnd = lN;
     return 0;
+}
+
+template <bool C4 = false>
+__device__ __forceinline__ int c5_merge_wave(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
+                                             uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint64_t* consumed,
+                                             MergeLds& W)
+{
+    const uint64_t kl = ((uint64_t)n + 3) / 4;
+    uint32_t carry = 0;
+    uint64_t lN = 0;
+    const int bad = c5_merge_range<C4>(in, total, dS, dM, dLl, out, n, 0u, n, 0, 0, 0, carry, &lN, W);
+    if (bad) return bad;
+    *consumed = kl + dS + dM + dLl + lN;
+    return 0;
+}
+
+// Sum (mod 2^16) of the deltas the samples of a range decode to -- order-free, so it is a plain
+// reduction over the range's stretches of the S / M / class-3 streams: S nibbles [s0, s1) at ps
+// (low nibble first), M bytes [m0, m1) at pm, class-3 pairs [l0, l1) at pl / ph.  Wave-uniform.
+template <bool C4 = false>
+__device__ inline uint32_t c5_range_delta_sum(const uint8_t* __restrict__ in, uint64_t ps, uint64_t pm, uint64_t pl,
+                                              uint64_t ph, uint64_t s0, uint64_t s1, uint64_t m0, uint64_t m1,
+                                              uint64_t l0, uint64_t l1)
+{
+    using CO = ClassOffsets<C4>;
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t acc = 0;
+    // S: bytes [s0 / 2, (s1 + 1) / 2), nibble i of the range in byte i / 2
+    {
+        const uint64_t b0 = ps + (s0 >> 1), b1 = ps + ((s1 + 1) >> 1);
+        for (uint64_t blk = (b0 & ~(uint64_t)15) + 16u * lane; blk < b1; blk += 1024) {
+            const uint4 v = gld<uint4>(in + blk);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint64_t nib0 = 2 * (blk + j - ps);  // this byte's low nibble index
+                const uint32_t by = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                if (nib0 >= s0 && nib0 < s1) acc += zz_dec16((uint16_t)((by & 15u) + CO::o1));
+                if (nib0 + 1 >= s0 && nib0 + 1 < s1) acc += zz_dec16((uint16_t)((by >> 4) + CO::o1));
+            }
+        }
+    }
+    {
+        const uint64_t b0 = pm + m0, b1 = pm + m1;
+        for (uint64_t blk = (b0 & ~(uint64_t)15) + 16u * lane; blk < b1; blk += 1024) {
+            const uint4 v = gld<uint4>(in + blk);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint64_t p = blk + j;
+                if (p >= b0 && p < b1) acc += zz_dec16((uint16_t)(((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) + CO::o2));
+            }
+        }
+    }
+    for (uint64_t i = l0 + lane; i < l1; i += 64)
+        acc += zz_dec16((uint16_t)(((uint32_t)gb(in + pl + i) | ((uint32_t)gb(in + ph + i) << 8)) + CO::o3));
+    return wave_sum(acc & 0xFFFFu) & 0xFFFFu;
+}
+
+// Class counts (S, M, class 3) of the samples in [t0, t1) from their keys (2 bits per sample, 16
+// samples per key word; codes past n are not samples), wave-uniform.
+__device__ inline void c5_class_counts(const uint8_t* __restrict__ in, uint32_t n, uint32_t t0, uint32_t t1,
+                                       uint32_t& cS, uint32_t& cM, uint32_t& cL)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t s = 0, m = 0, l = 0;
+    for (uint32_t t = t0 + 16u * lane; t < t1; t += 1024u) {
+        const uint32_t nK = (n - t + 3) / 4 < 4u ? (n - t + 3) / 4 : 4u;
+        uint32_t kw = 0;
+        if (nK == 4) {
+            kw = ld32u(in + (t >> 2));
+        } else {
+            for (uint32_t b = 0; b < nK; b++) kw |= (uint32_t)gb(in + (t >> 2) + b) << (8u * b);
+        }
+        const uint32_t nv = n - t;
+        if (nv < 16) kw &= (1u << (2u * nv)) - 1u;
+        const uint32_t lo = kw & 0x55555555u, hi = (kw >> 1) & 0x55555555u;
+        s += (uint32_t)__builtin_popcount(lo & ~hi);
+        m += (uint32_t)__builtin_popcount(hi & ~lo);
+        l += (uint32_t)__builtin_popcount(lo & hi);
+    }
+    cS = wave_sum(s);
+    cM = wave_sum(m);
+    cL = wave_sum(l);
 }
 
 }  // namespace pgn

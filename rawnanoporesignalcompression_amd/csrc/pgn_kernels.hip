@@ -415,6 +415,88 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void de
     P.flush();
 }
 
+// Small batches (the per-chunk calls): one workgroup of kMergeWaves waves per chunk.  Wave w takes
+// about 1/kMergeWaves of the chunk's 1,024-sample steps.  The class counts of every range (from its
+// keys) place each range in the S / M / class-3 streams; the delta sums of the ranges before a
+// wave's own (an order-free reduction over their stream bytes) give its running sum at entry; then
+// the waves merge their ranges at once.  Same statuses as dec_merge_kernel.
+constexpr int kMergeWaves = 16;
+constexpr size_t kMergeWgMaxChunks = 64;  // batches up to this many chunks use it
+__global__ __launch_bounds__(64 * kMergeWaves) void dec_merge_wg_kernel(DecArgs a)
+{
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    if (a.status[c] != PGN_OK) return;
+    __shared__ MergeLds Wv[kMergeWaves];
+    __shared__ uint32_t cnt[kMergeWaves][3];
+    __shared__ uint32_t sums[kMergeWaves];
+    __shared__ uint32_t badAny;
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t lane = (uint32_t)lane_id();
+    const DecUnit* d = a.units + g * kStreams;
+    uint64_t total = 0;
+    int st = PGN_OK;
+    for (int s = 0; s < kStreams; s++) {
+        if (d[s].dres < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
+        total += d[s].cs;
+    }
+    if (st != PGN_OK) {  // the same for every wave of the workgroup
+        if (threadIdx.x == 0) a.status[c] = st;
+        return;
+    }
+    const uint32_t n = a.sampleCounts[c];
+    const uint8_t* in = a.inter + g * kChunkInterBytes;
+    int16_t* out = a.samples + a.sampleOffsets[c];
+    const uint64_t dS = (uint64_t)d[1].dres, dM = (uint64_t)d[2].dres, dLl = (uint64_t)d[3].dres;
+    const uint64_t kl = ((uint64_t)n + 3) / 4;
+    const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
+    const uint32_t steps = (n + kSplitStep - 1) / kSplitStep;
+    const uint32_t s0 = (uint32_t)((uint64_t)steps * w / kMergeWaves), s1 = (uint32_t)((uint64_t)steps * (w + 1) / kMergeWaves);
+    const uint32_t t0 = s0 * kSplitStep, t1 = s1 * kSplitStep < n ? s1 * kSplitStep : n;
+    if (threadIdx.x == 0) badAny = kl > total ? 1u : 0u;  // the keys alone run past the streams
+    uint32_t cS = 0, cM = 0, cL = 0;
+    if (kl <= total) c5_class_counts(in, n, t0, t1, cS, cM, cL);
+    if (lane == 0) {
+        cnt[w][0] = cS;
+        cnt[w][1] = cM;
+        cnt[w][2] = cL;
+    }
+    __syncthreads();
+    uint64_t sN0 = 0, mN0 = 0, lN0 = 0, lTot = 0;
+    for (uint32_t v = 0; v < (uint32_t)kMergeWaves; v++) {
+        if (v < w) {
+            sN0 += cnt[v][0];
+            mN0 += cnt[v][1];
+            lN0 += cnt[v][2];
+        }
+        lTot += cnt[v][2];
+    }
+    const uint64_t sN1 = sN0 + cS, mN1 = mN0 + cM, lN1 = lN0 + cL;
+    // my range's stream bytes must lie inside the intermediate (else the one-wave merge fails too)
+    const bool inside = ps + ((sN1 + 1) >> 1) <= total && pm + mN1 <= total && pl + lN1 <= total && ph + lN1 <= total;
+    uint32_t sum = 0;
+    if (inside && kl <= total) sum = c5_range_delta_sum(in, ps, pm, pl, ph, sN0, sN1, mN0, mN1, lN0, lN1);
+    if (lane == 0) {
+        sums[w] = sum;
+        if (!inside) atomicOr(&badAny, 1u);
+    }
+    __syncthreads();
+    int bad = badAny != 0;
+    if (!bad) {
+        uint32_t carry = 0;
+        for (uint32_t v = 0; v < w; v++) carry += sums[v];
+        uint64_t lEnd = 0;
+        bad = c5_merge_range<false>(in, total, dS, dM, dLl, out, n, t0, t1, sN0, mN0, lN0, carry, &lEnd, Wv[w]);
+        if (bad && lane == 0) atomicOr(&badAny, 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (badAny) a.status[c] = PGN_ERR_CORRUPT;
+        else a.status[c] = (ph + lTot != total) ? PGN_ERR_REMAINING : PGN_OK;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // VBZ (pod5::compress_signal / decompress_signal, signal_compression.cpp:37-141): split -> one
 // zstd frame per chunk -> copy into place; parse -> zstd decode -> svb16 merge.  The per-chunk
@@ -1023,8 +1105,10 @@ struct pgn_ctx {
     DecUnit* lastUnits = nullptr;  // decode records of the last pass (diagnostics)
     uint32_t* queues = nullptr;    // one work counter per sub-batch pass
     size_t nQueues = 0;
-    // host-call staging (device buffers)
+    // host-call staging: a device buffer and its pinned host mirror (same layout), so a per-chunk
+    // call is one upload, the launches and one download
     uint8_t* stage = nullptr;
+    uint8_t* hstage = nullptr;
     size_t stageBytes = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // two-stream pipeline over sub-batches (launch_encode / launch_decode): the side stream runs the
@@ -1189,6 +1273,7 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->decChunks);
     (void)hipFree(c->queues);
     (void)hipFree(c->stage);
+    if (c->hstage) (void)hipHostFree(c->hstage);
     (void)hipFree(c->prof);
     if (c->scanStream) (void)hipStreamSynchronize(c->scanStream);
     (void)hipFree(c->largeList);
@@ -1402,8 +1487,13 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
     HIPCHK(hipEventRecord(c->ev[0], s));
     rc = ensure_queues(c, passes, s);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(c->evFork, s));
-    HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
+    // the split of pass p + 1 runs on the side stream beside pass p's zstd kernel; a single pass
+    // stays on the caller's stream (no fork, no cross-stream events)
+    const hipStream_t sideS = passes > 1 ? c->side : s;
+    if (passes > 1) {
+        HIPCHK(hipEventRecord(c->evFork, s));
+        HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
+    }
     const size_t bufBytes = G * (kChunkStreamBytes + kChunkFrameBytes + 2 * 4 * kStreams);
     EncArgs a;
     a.nchunks = nchunks;
@@ -1437,14 +1527,16 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
         a.base = p * G;
         a.queue = c->queues + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(c->side, c->evFree[b], 0));
-        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
-        else hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
-        HIPCHK(hipEventRecord(c->evStage[b], c->side));
-        HIPCHK(hipStreamWaitEvent(s, c->evStage[b], 0));
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        else hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        if (passes > 1) {
+            HIPCHK(hipEventRecord(c->evStage[b], c->side));
+            HIPCHK(hipStreamWaitEvent(s, c->evStage[b], 0));
+        }
         hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
         else hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-        HIPCHK(hipEventRecord(c->evFree[b], s));
+        if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], s));
     }
     HIPCHK(hipGetLastError());
     return PGN_OK;
@@ -1469,8 +1561,13 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     HIPCHK(hipEventRecord(c->ev[2], s));
     rc = ensure_queues(c, passes, s);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(c->evFork, s));
-    HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
+    // the merge of pass p runs on the side stream beside pass p + 1's zstd kernel; a single pass
+    // stays on the caller's stream
+    const hipStream_t sideS = passes > 1 ? c->side : s;
+    if (passes > 1) {
+        HIPCHK(hipEventRecord(c->evFork, s));
+        HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
+    }
     const size_t bufBytes = G * (kChunkInterBytes + kStreams * sizeof(DecUnit));
     DecArgs a;
     a.nchunks = nchunks;
@@ -1505,15 +1602,21 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         else hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-        HIPCHK(hipEventRecord(c->evStage[b], s));
-        HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
-        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
-        else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, c->side, a);
-        HIPCHK(hipEventRecord(c->evFree[b], c->side));
+        if (passes > 1) {
+            HIPCHK(hipEventRecord(c->evStage[b], s));
+            HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
+        }
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        else if (G <= kMergeWgMaxChunks)  // few chunks: one workgroup of kMergeWaves waves per chunk
+            hipLaunchKernelGGL(dec_merge_wg_kernel, dim3((unsigned)G), dim3(64 * kMergeWaves), 0, sideS, a);
+        else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], c->side));
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->evJoin, c->side));
-    HIPCHK(hipStreamWaitEvent(s, c->evJoin, 0));
+    if (passes > 1) {
+        HIPCHK(hipEventRecord(c->evJoin, c->side));
+        HIPCHK(hipStreamWaitEvent(s, c->evJoin, 0));
+    }
     return PGN_OK;
 }
 
@@ -1943,10 +2046,15 @@ int pgn_synth_reads_device(pgn_ctx* c, size_t nreads, uint64_t seed, uint64_t fi
 static int ensure_stage(pgn_ctx* c, size_t bytes)
 {
     if (bytes <= c->stageBytes) return PGN_OK;
+    wait_last_host(c);
     (void)hipFree(c->stage);
+    if (c->hstage) (void)hipHostFree(c->hstage);
     c->stage = nullptr;
+    c->hstage = nullptr;
+    c->stageBytes = 0;
     size_t b = align_up(bytes, 1 << 20);
     HIPCHK(hipMalloc(&c->stage, b));
+    HIPCHK(hipHostMalloc((void**)&c->hstage, b, hipHostMallocDefault));
     c->stageBytes = b;
     return PGN_OK;
 }
@@ -1958,6 +2066,9 @@ struct StageHdr {
     uint64_t stats[PGN_STATS_PER_CHUNK];
 };
 
+// One chunk from host memory: header and samples staged in the pinned mirror and uploaded in one
+// copy; the header and the destination area (cap bytes) come back in two queued copies and one
+// wait; the blob leaves the pinned mirror by memcpy.
 static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap,
                            size_t* out_size)
 {
@@ -1971,22 +2082,22 @@ static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t
     uint8_t* dh = c->stage;
     uint8_t* din = c->stage + hdrB;
     uint8_t* dout = din + inB;
-    StageHdr h{};
-    h.off0 = 0;
-    h.outOff = 0;
-    h.outCap = cap;
-    h.count = (uint32_t)n;
-    HIPCHK(hipMemcpyAsync(dh, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
-    if (n) HIPCHK(hipMemcpyAsync(din, samples, 2 * n, hipMemcpyHostToDevice, c->stream));
+    StageHdr* hh = (StageHdr*)c->hstage;
+    *hh = StageHdr{};
+    hh->outCap = cap;
+    hh->count = (uint32_t)n;
+    if (n) memcpy(c->hstage + hdrB, samples, 2 * n);
+    HIPCHK(hipMemcpyAsync(dh, c->hstage, hdrB + 2 * n, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
     rc = launch_encode(c, codec, 1, (const int16_t*)din, &d->off0, &d->count, dout, &d->outOff, &d->outCap,
                        &d->outSize, &d->status, d->stats, c->stream, n ? (uint32_t)n : 1u);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(&h, dh, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->hstage, dh, sizeof(StageHdr), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->hstage + hdrB + inB, dout, cap, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    *out_size = (size_t)h.outSize;
-    if (h.status != PGN_OK) return h.status;
-    HIPCHK(hipMemcpy(dst, dout, (size_t)h.outSize, hipMemcpyDeviceToHost));
+    *out_size = (size_t)hh->outSize;
+    if (hh->status != PGN_OK) return hh->status;
+    memcpy(dst, c->hstage + hdrB + inB, (size_t)hh->outSize);
     return PGN_OK;
 }
 
@@ -2002,21 +2113,21 @@ static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t l
     uint8_t* dh = c->stage;
     uint8_t* din = c->stage + hdrB;
     int16_t* dout = (int16_t*)(din + inB);
-    StageHdr h{};
-    h.inOff = 0;
-    h.inSize = len;
-    h.off0 = 0;
-    h.count = (uint32_t)n;
-    HIPCHK(hipMemcpyAsync(dh, &h, sizeof(h), hipMemcpyHostToDevice, c->stream));
-    if (len) HIPCHK(hipMemcpyAsync(din, src, len, hipMemcpyHostToDevice, c->stream));
+    StageHdr* hh = (StageHdr*)c->hstage;
+    *hh = StageHdr{};
+    hh->inSize = len;
+    hh->count = (uint32_t)n;
+    if (len) memcpy(c->hstage + hdrB, src, len);
+    HIPCHK(hipMemcpyAsync(dh, c->hstage, hdrB + len, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
     rc = launch_decode(c, codec, 1, din, &d->inOff, &d->inSize, dout, &d->off0, &d->count, &d->status, c->stream,
                        n ? (uint32_t)n : 1u);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(&h, dh, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->hstage, dh, sizeof(StageHdr), hipMemcpyDeviceToHost, c->stream));
+    if (n) HIPCHK(hipMemcpyAsync(c->hstage + hdrB + inB, dout, 2 * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (h.status != PGN_OK) return h.status;
-    if (n) HIPCHK(hipMemcpy(dst, dout, 2 * n, hipMemcpyDeviceToHost));
+    if (hh->status != PGN_OK) return hh->status;
+    if (n) memcpy(dst, c->hstage + hdrB + inB, 2 * n);
     return PGN_OK;
 }
 
