@@ -278,6 +278,141 @@ __device__ __forceinline__ void c5_split_wave(const int16_t* __restrict__ x, uin
 }
 
 // ---------------------------------------------------------------------------------------------
+// Split of a step range [t0, t1) (small batches: the waves of a workgroup share one chunk).  The
+// range's streams start at S nibble pS and M / class-3 bytes pM / pL (the class counts of the
+// ranges before it); its windows start at the 16-byte block holding that first entry, and the
+// entries in front of it ("lead", the ranges before) are never written.  The S byte shared with the
+// range before (pS odd) and a trailing half byte are left to the caller, with the nibbles it needs:
+// firstNib (the range's first nibble when pS is odd) and lastNib (its last when its end is odd);
+// 0xFF for none.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void bwin_flush_lead(uint8_t* W, uint32_t& fill, uint8_t* out, uint32_t& gpos, uint32_t& lead)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t nblk = fill >> 4, tail = fill & 15u;
+    for (uint32_t b = lane; b < nblk; b += 64) {
+        if (b == 0 && lead) {
+            for (uint32_t k = lead; k < 16; k++) gst<uint8_t>(out + gpos + k, W[k]);
+        } else {
+            gst<uint4>(out + gpos + 16u * b, *(const uint4*)(W + 16u * b));
+        }
+    }
+    if (nblk) {
+        const uint8_t v = W[16u * nblk + (lane & 15u)];
+        if (lane < tail) W[lane] = v;
+        lead = 0;
+    }
+    gpos += 16u * nblk;
+    fill = tail;
+}
+__device__ __forceinline__ void nwin_flush_lead(uint8_t* W, uint32_t& fill, uint8_t* out, uint32_t& gpos, uint32_t& lead)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t nblk = fill >> 5, tail = fill & 31u;
+    for (uint32_t b = lane; b < nblk; b += 64) {
+        if (b == 0 && lead) {  // bytes whose both nibbles are the range's (the shared one is the caller's)
+            for (uint32_t k = (lead + 1) >> 1; k < 16; k++) gst<uint8_t>(out + gpos + k, (uint8_t)(W[2 * k] | (W[2 * k + 1] << 4)));
+        } else {
+            const uint4 a = *(const uint4*)(W + 32u * b), c = *(const uint4*)(W + 32u * b + 16u);
+            uint4 o;
+            o.x = pack_nibbles(a.x) | (pack_nibbles(a.y) << 16);
+            o.y = pack_nibbles(a.z) | (pack_nibbles(a.w) << 16);
+            o.z = pack_nibbles(c.x) | (pack_nibbles(c.y) << 16);
+            o.w = pack_nibbles(c.z) | (pack_nibbles(c.w) << 16);
+            gst<uint4>(out + gpos + 16u * b, o);
+        }
+    }
+    if (nblk) {
+        const uint8_t v = W[32u * nblk + (lane & 31u)];
+        if (lane < tail) W[lane] = v;
+        lead = 0;
+    }
+    gpos += 16u * nblk;
+    fill = tail;
+}
+
+template <bool C4 = false>
+__device__ inline void c5_split_range(const int16_t* __restrict__ x, uint32_t n, uint32_t t0, uint32_t t1,
+                                      const C5Streams& st, uint32_t pS, uint32_t pM, uint32_t pL, SplitLds& W,
+                                      uint32_t& firstNib, uint32_t& lastNib)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t fS = pS & 31u, fM = pM & 15u, fL = pL & 15u, fH = fL;  // window fills, lead included
+    uint32_t gS = (pS >> 1) & ~15u, gM = pM & ~15u, gL = pL & ~15u, gH = gL;
+    uint32_t leadS = fS, leadM = fM, leadL = fL, leadH = fL;
+    uint32_t prevX = t0 ? (uint32_t)(uint16_t)__builtin_amdgcn_readfirstlane((int)gld<uint16_t>(x + t0 - 1)) : 0u;
+    firstNib = 0xFFu;
+    lastNib = 0xFFu;
+    uint4 na = make_uint4(0u, 0u, 0u, 0u), nb = na;
+    if (t0 + kSplitStep <= n) {
+        na = gld<uint4>(x + t0 + 16u * lane);
+        nb = gld<uint4>(x + t0 + 16u * lane + 8);
+    }
+    for (uint32_t t = t0; t < t1; t += kSplitStep) {
+        const bool full = t + kSplitStep <= n;
+        const uint4 ca = na, cb = nb;
+        if (t + kSplitStep < t1 && t + 2 * kSplitStep <= n) {
+            na = gld<uint4>(x + t + kSplitStep + 16u * lane);
+            nb = gld<uint4>(x + t + kSplitStep + 16u * lane + 8);
+        }
+        const uint32_t kw = full ? split_step<true, C4>(ca, cb, x, n, t, W, fS, fM, fL, prevX)
+                                 : split_step<false, C4>(ca, cb, x, n, t, W, fS, fM, fL, prevX);
+        fH = fL;
+        const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
+        uint8_t* kout = st.K + (t >> 2);
+        if (4u * lane + 4u <= nK) gst<uint32_t>(kout + 4u * lane, kw);
+        else for (uint32_t b = 4u * lane; b < nK; b++) gst<uint8_t>(kout + b, (uint8_t)(kw >> (8u * (b - 4u * lane))));
+        lds_sync();
+        if (firstNib == 0xFFu && (pS & 1u) && fS > leadS) firstNib = W.S[leadS];
+        nwin_flush_lead(W.S, fS, st.S, gS, leadS);
+        bwin_flush_lead(W.M, fM, st.M, gM, leadM);
+        bwin_flush_lead(W.L, fL, st.Ll, gL, leadL);
+        bwin_flush_lead(W.H, fH, st.Lh, gH, leadH);
+        lds_sync();
+    }
+    // tails: whole bytes of the range only
+    const uint32_t nbS = (fS + 1) / 2;
+    for (uint32_t j = lane; j < nbS; j += 64) {
+        if (2 * j < leadS || 2 * j + 1 >= fS) continue;  // the lead's, the shared byte, or a trailing half byte
+        gst<uint8_t>(st.S + gS + j, (uint8_t)(W.S[2 * j] | (W.S[2 * j + 1] << 4)));
+    }
+    if (fS > leadS && (fS & 1u)) lastNib = W.S[fS - 1];
+    for (uint32_t j = leadM + lane; j < fM; j += 64) gst<uint8_t>(st.M + gM + j, W.M[j]);
+    for (uint32_t j = leadL + lane; j < fL; j += 64) {
+        gst<uint8_t>(st.Ll + gL + j, W.L[j]);
+        gst<uint8_t>(st.Lh + gH + j, W.H[j]);
+    }
+    lds_sync();
+}
+
+// Class counts (S, M, class 3) of the samples [t0, t1) of a chunk, from the samples (the delta of
+// sample 0 is from 0), wave-uniform.
+template <bool C4 = false>
+__device__ inline void c5_split_counts(const int16_t* __restrict__ x, uint32_t n, uint32_t t0, uint32_t t1, uint32_t& cS,
+                                       uint32_t& cM, uint32_t& cL)
+{
+    using CO = ClassOffsets<C4>;
+    const uint32_t lane = (uint32_t)lane_id();
+    uint32_t s = 0, m = 0, l = 0;
+    for (uint32_t t = t0 + 16u * lane; t < t1; t += 1024u) {
+        uint32_t prev = t ? (uint32_t)gld<uint16_t>(x + t - 1) : 0u;
+        const uint32_t e = t + 16u < t1 ? t + 16u : t1;
+        for (uint32_t i = t; i < e; i++) {
+            const uint32_t v = gld<uint16_t>(x + i);
+            const uint32_t d = (v - prev) & 0xFFFFu;
+            const uint32_t z = ((d << 1) ^ (0u - (d >> 15))) & 0xFFFFu;
+            prev = v;
+            s += (z >= 1u && z <= CO::t1) ? 1u : 0u;
+            m += (z > CO::t1 && z <= CO::t2) ? 1u : 0u;
+            l += (z > CO::t2) ? 1u : 0u;
+        }
+    }
+    cS = wave_sum(s);
+    cM = wave_sum(m);
+    cL = wave_sum(l);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Merge over the reference's concatenated intermediate buffer (see oracle c5_merge): stream starts at
 // keys_length = ceil(n/4), then +dS, +dM, +dLl; a read past `total` is the reference's UB -> error.
 // Per 1024-sample step the class counts come from the key bytes, the step's S/M/L bytes are staged

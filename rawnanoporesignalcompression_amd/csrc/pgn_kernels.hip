@@ -188,6 +188,86 @@ __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
     P.flush();
 }
 
+// Small batches (the per-chunk calls): one workgroup of kSplitWaves waves per chunk.  Wave w takes
+// about 1/kSplitWaves of the chunk's 1,024-sample steps; the class counts of every range (from the
+// samples) place each range in the S / M / class-3 streams; the waves split their ranges at once;
+// then the S bytes shared by two ranges (an odd nibble start) and a trailing half byte are written
+// from the nibbles the waves handed over.
+constexpr int kSplitWaves = 16;
+constexpr size_t kSplitWgMaxChunks = 64;  // batches up to this many chunks use it
+__global__ __launch_bounds__(64 * kSplitWaves) void enc_split_wg_kernel(EncArgs a)
+{
+    const size_t g = blockIdx.x;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    __shared__ SplitLds Wv[kSplitWaves];
+    __shared__ uint32_t cnt[kSplitWaves][3];
+    __shared__ uint32_t nibs[kSplitWaves][2];
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t n = a.sampleCounts[c];
+    uint32_t* sz = a.sizes + g * kStreams;
+    if (n > kPassSamples) {  // the large-chunk pass takes it
+        if (threadIdx.x == 0) {
+            sz[0] = ~0u;
+            a.status[c] = PGN_ERR_UNSUPPORTED;
+            a.outSizes[c] = 0;
+        }
+        return;
+    }
+    const int16_t* x = a.samples + a.sampleOffsets[c];
+    uint8_t* base = a.streams + g * kChunkStreamBytes;
+    const C5Streams st{base + stream_off(0), base + stream_off(1), base + stream_off(2), base + stream_off(3),
+                       base + stream_off(4)};
+    const uint32_t steps = (n + kSplitStep - 1) / kSplitStep;
+    const uint32_t s0 = steps * w / kSplitWaves, s1 = steps * (w + 1) / kSplitWaves;
+    const uint32_t t0 = s0 * kSplitStep, t1 = s1 * kSplitStep < n ? s1 * kSplitStep : n;
+    uint32_t cS = 0, cM = 0, cL = 0;
+    c5_split_counts(x, n, t0, t1, cS, cM, cL);
+    if (lane == 0) {
+        cnt[w][0] = cS;
+        cnt[w][1] = cM;
+        cnt[w][2] = cL;
+    }
+    __syncthreads();
+    uint32_t pS = 0, pM = 0, pL = 0, tS = 0, tM = 0, tL = 0;
+    for (uint32_t v = 0; v < (uint32_t)kSplitWaves; v++) {
+        if (v < w) {
+            pS += cnt[v][0];
+            pM += cnt[v][1];
+            pL += cnt[v][2];
+        }
+        tS += cnt[v][0];
+        tM += cnt[v][1];
+        tL += cnt[v][2];
+    }
+    uint32_t firstNib = 0xFFu, lastNib = 0xFFu;
+    if (t0 < t1) c5_split_range(x, n, t0, t1, st, pS, pM, pL, Wv[w], firstNib, lastNib);
+    if (lane == 0) {
+        nibs[w][0] = firstNib;
+        nibs[w][1] = lastNib;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // the S bytes two ranges share, then a trailing half byte (its high nibble zero)
+        uint32_t at = 0, lastOwner = ~0u;
+        for (uint32_t v = 0; v < (uint32_t)kSplitWaves; v++) {
+            if (cnt[v][0] == 0) continue;
+            if ((at & 1u) && lastOwner != ~0u)
+                gst<uint8_t>(st.S + (at >> 1), (uint8_t)(nibs[lastOwner][1] | (nibs[v][0] << 4)));
+            at += cnt[v][0];
+            lastOwner = v;
+        }
+        // the stream's odd end (a byte of its own: with an odd start the last range's count is even)
+        if ((at & 1u) && lastOwner != ~0u) gst<uint8_t>(st.S + (at >> 1), (uint8_t)nibs[lastOwner][1]);
+        sz[0] = (n + 3) / 4;
+        sz[1] = (tS + 1) / 2;
+        sz[2] = tM;
+        sz[3] = tL;
+        sz[4] = tL;
+    }
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void enc_zstd_kernel(EncArgs a)
 {
     const int lane = lane_id();
@@ -1528,6 +1608,8 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
         a.queue = c->queues + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(c->side, c->evFree[b], 0));
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        else if (G <= kSplitWgMaxChunks)  // few chunks: one workgroup of kSplitWaves waves per chunk
+            hipLaunchKernelGGL(enc_split_wg_kernel, dim3((unsigned)G), dim3(64 * kSplitWaves), 0, sideS, a);
         else hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         if (passes > 1) {
             HIPCHK(hipEventRecord(c->evStage[b], c->side));

@@ -239,3 +239,65 @@ def test_huffman_stress_signals_identical(codec):
     torch.cuda.synchronize()
     assert (st.cpu().numpy() == 0).all()
     assert np.array_equal(out.cpu().numpy()[: counts.sum()], np.concatenate([x for _, x in blobs]))
+
+
+def test_small_batches_take_the_workgroup_split_and_merge(codec):
+    """Batches of up to 64 chunks split and merge each chunk with a 16-wave workgroup (range class
+    counts, shared S bytes at odd nibble starts, order-free delta sums); larger batches with one wave
+    per chunk.  Both give the oracle's blobs and the same samples and statuses, corrupted blobs
+    included."""
+    import torch
+
+    rng = np.random.default_rng(64)
+    lens = rng.integers(0, 262145, 65).astype(np.int32)
+    lens[:6] = [0, 1, 1023, 1024, 1025, 16 * 1024 + 7]
+    reads = [O.synth_read(5000 + i, int(n)) if i % 3 else
+             np.clip(rng.normal(0, 10 + 20 * (i % 5), int(n)), -32768, 32767).astype(np.int16)
+             for i, n in enumerate(lens)]
+    flat = np.concatenate(reads)
+    dev = torch.device("cuda", 0)
+    samples = torch.from_numpy(flat).to(dev)
+    counts = torch.from_numpy(lens).to(dev)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lens.astype(np.int64))[:-1]])).to(dev)
+    whole = codec.compress_batch(samples, offs, counts)          # 65 chunks: one wave per chunk
+    parts = [codec.compress_batch(samples, offs[a:b], counts[a:b]) for a, b in ((0, 33), (33, 65))]
+    torch.cuda.synchronize()
+    wb, wo, ws = whole.blobs.cpu().numpy(), whole.offsets.cpu().numpy(), whole.sizes.cpu().numpy()
+    blobs = []
+    for (a, b), p in zip(((0, 33), (33, 65)), parts):
+        pb, po, ps = p.blobs.cpu().numpy(), p.offsets.cpu().numpy(), p.sizes.cpu().numpy()
+        for i in range(b - a):
+            blob = pb[po[i]:po[i] + ps[i]].tobytes()
+            assert blob == wb[wo[a + i]:wo[a + i] + ws[a + i]].tobytes(), a + i
+            blobs.append(blob)
+    for i in list(range(0, 65, 4)) + [1, 2, 3, 4, 5]:
+        rc, ref, _ = O.c5_compress(reads[i])
+        assert rc == 0 and blobs[i] == ref, i
+    # decode: valid and corrupted blobs, one batch of 65 vs two of <= 64
+    bad = [bytearray(b) for b in blobs]
+    for i in range(0, 65, 5):
+        if len(bad[i]) > 40:
+            bad[i][len(bad[i]) // 2] ^= 0x5A
+    for i in range(2, 65, 7):
+        bad[i] = bad[i][:-3] if len(bad[i]) > 50 else bad[i]
+    data = b"".join(bytes(b) for b in bad)
+    bsz = np.array([len(b) for b in bad], np.int64)
+    boff = np.concatenate([[0], np.cumsum(bsz)[:-1]]).astype(np.int64)
+    din = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
+    ob, sb = torch.from_numpy(boff).to(dev), torch.from_numpy(bsz).to(dev)
+    out_w, _, st_w = codec.decompress_batch(din, ob, sb, counts)
+    res = [codec.decompress_batch(din, ob[a:b], sb[a:b], counts[a:b]) for a, b in ((0, 33), (33, 65))]
+    torch.cuda.synchronize()
+    st_p = torch.cat([r[2] for r in res]).cpu().numpy()
+    assert np.array_equal(st_w.cpu().numpy(), st_p)
+    ow = out_w.cpu().numpy()
+    so = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    for k, (a, b) in enumerate(((0, 33), (33, 65))):
+        op = res[k][0].cpu().numpy()
+        base = so[a]
+        for i in range(a, b):
+            rc, ref = O.c5_decompress(bytes(bad[i]), int(lens[i]))
+            assert st_p[i] == rc, (i, rc, st_p[i])
+            if rc == 0:
+                assert np.array_equal(op[so[i] - base:so[i + 1] - base], ref), i
+                assert np.array_equal(ow[so[i]:so[i + 1]], ref), i

@@ -193,3 +193,34 @@ def test_two_rank_transcode_matches_single_rank(codec, tmp_path, dst):
         return b.replace(b[8:24], bytes(16))
 
     assert unmarked(two) == unmarked(one)
+
+
+def test_transcode_uniform_noise_rows_fail_without_fault(codec, tmp_path):
+    """Rows the C5 codec refuses (uniform noise exceeds max(2n + 26, 1024), compressor.h:39-45) fail
+    the transcode with PGN_ERR_DST_TOO_SMALL, whatever rows surround them; the device packing only
+    counts successful rows, so nothing is written past the packed column."""
+    from rawnanoporesignalcompression_amd import PGNanoError
+    from rawnanoporesignalcompression_amd.pod5_file import Pod5File, SignalTable, transcode_pod5, write_pod5
+
+    import _oracle as O
+
+    rng = np.random.default_rng(5)
+    xs = [O.synth_read(700 + i, 60000) for i in range(5)]
+    xs += [rng.integers(-32768, 32768, 90000).astype(np.int16) for _ in range(30)]
+    xs += [O.synth_read(800 + i, 50000) for i in range(5)]
+    data = np.concatenate([x.view(np.uint8) for x in xs])
+    offs = np.concatenate([[0], np.cumsum([2 * x.size for x in xs])]).astype(np.uint64)
+    ids = rng.integers(0, 256, (len(xs), 16)).astype(np.uint8)
+    src = str(tmp_path / "noise.pod5")
+    write_pod5(src, SignalTable(ids, np.array([x.size for x in xs], np.uint32), offs, data, "uncompressed"))
+    with pytest.raises(PGNanoError) as e:
+        transcode_pod5(src, str(tmp_path / "never.pod5"), "pgnano", codec=codec)
+    assert e.value.status == 1  # PGN_ERR_DST_TOO_SMALL
+    # the context still works: the same file to VBZ (which takes noise) and back
+    vbz = str(tmp_path / "noise_vbz.pod5")
+    transcode_pod5(src, vbz, "vbz", codec=codec)
+    back = str(tmp_path / "back.pod5")
+    transcode_pod5(vbz, back, "uncompressed", codec=codec)
+    with Pod5File(back) as f:
+        t = f.signal_table()
+        assert t.data.tobytes() == data.tobytes()
