@@ -34,44 +34,71 @@ __device__ __forceinline__ void hdbg(uint32_t tag, uint32_t a, uint32_t b, uint3
 }
 #endif
 
-// Reader over the lane's staged words: Wd = staged bits [wlo, wlo + 64), nxw = the word below it.
-struct StgBits {
+// Reader over the lane's staged words.  Wd holds the staged bits [32 (row + 1), 32 (row + 1) + 64) of
+// the round's window, u is the shift of the next codeword's tl-bit peek inside Wd (the codeword's top
+// bit is at local position u + tl + 32 (row + 1)), nxw is staged word `row` (the next refill).  A
+// refill check every two codewords keeps both peeks inside Wd (u >= tl after it; u < tl + 32 <= 43
+// so u + tl <= 54).  Rows below 0 read the decode table in front of the staging rows: only a path
+// that has left the stream's staged bits does that, and it never uses the bits.
+struct HufRd {
     uint64_t Wd;
-    int32_t wlo;
+    int32_t u;
+    int32_t row;
     uint32_t nxw;
 };
-__device__ __forceinline__ void stg_init(StgBits& r, int lane, int32_t x)  // x = q - b8 - tl
+__device__ __forceinline__ uint32_t stg_word(int32_t row, int lane)
+{
+    constexpr int32_t kStgFirst = (int32_t)(__builtin_offsetof(DecLds, stg) / 4);
+    return reinterpret_cast<const uint32_t*>(&sDec)[kStgFirst + 64 * row + lane];
+}
+__device__ __forceinline__ void rd_init(HufRd& r, int lane, int32_t x)  // x = q - b8 - tl
 {
     int32_t wi = x >> 5;
     wi = wi < 0 ? 0 : (wi > kStgWords - 2 ? kStgWords - 2 : wi);
-    r.wlo = 32 * wi;
     r.Wd = (uint64_t)sDec.stg[wi][lane] | ((uint64_t)sDec.stg[wi + 1][lane] << 32);
-    r.nxw = sDec.stg[wi > 0 ? wi - 1 : 0][lane];
+    r.u = x - 32 * wi;
+    r.row = wi - 1;
+    r.nxw = stg_word(r.row, lane);
 }
-// decode-table entry of the tl bits at local position x (one refill at most: tl <= 11 < 32)
-__device__ __forceinline__ uint32_t stg_entry(StgBits& r, int lane, int32_t x, uint32_t tmask)
+__device__ __forceinline__ void rd_refill(HufRd& r, int lane, int32_t tl)
 {
-    const bool rf = x < r.wlo;
+    const bool rf = r.u < tl;
     r.Wd = rf ? ((r.Wd << 32) | r.nxw) : r.Wd;
-    r.wlo = rf ? r.wlo - 32 : r.wlo;
-    r.nxw = sDec.stg[r.wlo >= 64 ? (r.wlo >> 5) - 1 : 0][lane];
-    return sDec.tab[(uint32_t)(r.Wd >> ((x - r.wlo) & 63)) & tmask];
+    r.u += rf ? 32 : 0;
+    r.row -= rf ? 1 : 0;
+    r.nxw = stg_word(r.row, lane);
 }
+// decode-table entry (symbol | nbBits << 8) of the next codeword
+__device__ __forceinline__ uint32_t rd_entry(const HufRd& r, uint32_t tmask)
+{
+    return sDec.tab[(uint32_t)(r.Wd >> r.u) & tmask];
+}
+__device__ __forceinline__ uint32_t rd_nbits(const HufRd& r, uint32_t tmask)
+{
+    return (uint32_t)(reinterpret_cast<const uint8_t*>(sDec.tab))[2u * ((uint32_t)(r.Wd >> r.u) & tmask) + 1u];
+}
+// z = u + 32 row: the next codeword's top position is z + (tl + b8 + 32)
+__device__ __forceinline__ int32_t rd_z(const HufRd& r) { return r.u + 32 * r.row; }
 
-// Two decode-table entries: the codeword at x and the one below it.  One refill check and one
-// staged-word prefetch serve both lookups: refilling whenever fewer than tl bits remain above the
-// window base keeps both peeks inside the 64-bit window (x - wlo < 32 + tl after a refill, so
-// x + tl <= wlo + 54).  Halves the per-symbol refill/prefetch cost of the unpredicated loops.
-__device__ __forceinline__ void stg_entry2(StgBits& r, int lane, int32_t x, uint32_t tmask, int32_t tl, uint32_t& e1,
-                                           uint32_t& e2)
+// Recorded codeword starts: the first kRecSyms starts at or below a lane's window top, as distances
+// below the top, one byte each (0xFF = none; a distance is at most tl - 1 + 19 * 11 < 255).
+constexpr int kRecSyms = 20;
+struct RecStarts {
+    uint32_t w[kRecSyms / 4];
+};
+// number of recorded starts before the one at distance d (-1: none recorded at d).  The distances
+// increase, so at most one byte matches; a word's lowest zero byte after the XOR is exact.
+__device__ __forceinline__ int32_t rec_index(const RecStarts& R, int32_t d)
 {
-    const bool rf = x - r.wlo < tl;
-    r.Wd = rf ? ((r.Wd << 32) | r.nxw) : r.Wd;
-    r.wlo = rf ? r.wlo - 32 : r.wlo;
-    r.nxw = sDec.stg[r.wlo >= 64 ? (r.wlo >> 5) - 1 : 0][lane];
-    e1 = sDec.tab[(uint32_t)(r.Wd >> ((x - r.wlo) & 63)) & tmask];
-    const int32_t x2 = x - (int32_t)(e1 >> 8);
-    e2 = sDec.tab[(uint32_t)(r.Wd >> ((x2 - r.wlo) & 63)) & tmask];
+    if (d < 0 || d > 254) return -1;
+    const uint32_t rep = (uint32_t)d * 0x01010101u;
+#pragma unroll
+    for (int i = 0; i < kRecSyms / 4; i++) {
+        const uint32_t x = R.w[i] ^ rep;
+        const uint32_t z = (x - 0x01010101u) & ~x & 0x80808080u;
+        if (z) return 4 * i + (int32_t)(__builtin_ctz(z) >> 3);
+    }
+    return -1;
 }
 
 // Returns false on a malformed section.  jt = the jump table's three stream sizes (l1 | l2 << 16,
@@ -124,72 +151,71 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             sDec.stg[4 * i + 2][lane] = nx[i].z;
             sDec.stg[4 * i + 3][lane] = nx[i].w;
         }
-        uint64_t bm0 = 0, bm1 = 0;  // boundary bitmap: bit d = codeword start at hi - d (d < 128)
         const int32_t nextT = T - 16 * kWinBits;
         if (ballot(nextT > 0)) {  // next round's bytes, in flight during this one
             base = round_base(nextT - j * kWinBits);
             round_load(nx, src, sl, base);
         }
         lds_sync();
-        // ---- pass A: speculative decode of (lo, hi]: symbol count c, exit q
+        // ---- pass A: speculative decode of (lo, hi]: symbol count c, exit q, the first kRecSyms
+        // codeword starts at or below hi (distances hi - q, one byte each; 0xFF = none)
         // lanes 1..15 start kOvBits above their window (inside the staged bytes: 8 * base + 32 *
         // kStgWords >= hi + 65), so the speculative path has usually merged with the true one by hi
-        // and the sync below finds the true entry among the recorded boundaries without a walk
-        int32_t q = (j == 0 || hi <= lo) ? hi : hi + kOvBits;
+        // and the sync below finds the true entry among the recorded starts without a walk.
+        // Positions are kept as z = q - K0 (the reader's u + 32 row).
+        const int32_t K0 = tli + b8 + 32;
+        const int32_t zHi = hi - K0, zLo = lo - K0;
         uint32_t c = 0;
+        RecStarts rec;
+        int32_t q;
         {
-            StgBits r;
-            stg_init(r, lane, q - b8 - tli);
-            while (ballot(q > hi)) {  // overlap: decoded, neither counted nor recorded
+            HufRd r;
+            rd_init(r, lane, ((j == 0 || hi <= lo) ? hi : hi + kOvBits) - b8 - tli);
+            while (ballot(rd_z(r) > zHi)) {  // overlap: decoded, neither counted nor recorded
                 P.count(1);
-                uint32_t e[2];
-                stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
+                rd_refill(r, lane, tli);
 #pragma unroll
-                for (int u = 0; u < 2; u++) q = q > hi ? q - (int32_t)(e[u] >> 8) : q;
+                for (int v = 0; v < 2; v++) {
+                    const uint32_t nb = rd_nbits(r, tmask);
+                    r.u -= rd_z(r) > zHi ? (int32_t)nb : 0;
+                }
             }
-            while (ballot(q > lo && hi - q < kBmpBits)) {
-                P.count(2);
-                uint32_t e[2];
-                stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
+            P.count(2);
 #pragma unroll
-                for (int u = 0; u < 2; u++) {  // the second entry is only used if the first was
-                    const bool act = q > lo && hi - q < kBmpBits;
-                    const int32_t d = hi - q;
-                    const uint64_t bit = 1ull << (d & 63);
-                    bm0 |= (act && d < 64) ? bit : 0ull;
-                    bm1 |= (act && d >= 64) ? bit : 0ull;
-                    q = act ? q - (int32_t)(e[u] >> 8) : q;
+            for (int i = 0; i < kRecSyms; i++) {  // the first kRecSyms codewords: recorded and counted
+                if ((i & 1) == 0) rd_refill(r, lane, tli);
+                const int32_t z = rd_z(r);
+                const bool act = z > zLo;
+                const uint32_t d = act ? (uint32_t)(zHi - z) : 0xFFu;
+                rec.w[i >> 2] = (i & 3) ? (rec.w[i >> 2] | (d << (8 * (i & 3)))) : d;
+                const uint32_t nb = rd_nbits(r, tmask);
+                r.u -= act ? (int32_t)nb : 0;
+                c += act ? 1u : 0u;
+            }
+            // every active lane has >= 4 * tl bits left: four symbols, lanes that are done frozen
+            while (ballot(rd_z(r) > zLo) && !ballot(rd_z(r) > zLo && rd_z(r) - zLo < 4 * tli)) {
+                P.count(3);
+                const bool act = rd_z(r) > zLo;
+#pragma unroll
+                for (int v = 0; v < 4; v++) {
+                    if ((v & 1) == 0) rd_refill(r, lane, tli);
+                    const uint32_t nb = rd_nbits(r, tmask);
+                    r.u -= act ? (int32_t)nb : 0;
+                }
+                c += act ? 4u : 0u;
+            }
+            while (ballot(rd_z(r) > zLo)) {
+                P.count(4);
+                rd_refill(r, lane, tli);
+#pragma unroll
+                for (int v = 0; v < 2; v++) {
+                    const bool act = rd_z(r) > zLo;
+                    const uint32_t nb = rd_nbits(r, tmask);
+                    r.u -= act ? (int32_t)nb : 0;
                     c += act ? 1u : 0u;
                 }
             }
-            // every active lane has >= 4 * tl bits left: four symbols without a bound check
-            while (ballot(q > lo) && !ballot(q > lo && q - lo < 4 * tli)) {
-                P.count(3);
-                const bool act = q > lo;
-                int32_t qq = q;
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    uint32_t e1, e2;
-                    stg_entry2(r, lane, qq - b8 - tli, tmask, tli, e1, e2);
-                    qq -= (int32_t)(e1 >> 8) + (int32_t)(e2 >> 8);
-                }
-                q = act ? qq : q;
-                c += act ? 4u : 0u;
-            }
-            while (ballot(q > lo)) {
-                P.count(4);
-#pragma unroll
-                for (int v = 0; v < 2; v++) {
-                    uint32_t e[2];
-                    stg_entry2(r, lane, q - b8 - tli, tmask, tli, e[0], e[1]);
-#pragma unroll
-                    for (int u = 0; u < 2; u++) {
-                        const bool act = q > lo;
-                        q = act ? q - (int32_t)(e[u] >> 8) : q;
-                        c += act ? 1u : 0u;
-                    }
-                }
-            }
+            q = rd_z(r) + K0;
         }
         P.mark(11);
         // ---- sync: true entries, symbol counts and exits
@@ -204,28 +230,20 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             if (need) {
                 int32_t p = entry;
                 uint32_t w = 0;
-                // a recorded boundary at p (none lies at or below lo: kBmpBits < kWinBits)
-                auto recorded = [&](int32_t pp) {
-                    const int32_t d = hi - pp;
-                    return d < kBmpBits && (((d < 64 ? (bm0 >> d) : (bm1 >> (d - 64))) & 1ull) != 0);
-                };
-                bool synced = recorded(p);
-                if (!synced && p > lo) {  // walk the true path until it meets a recorded boundary
-                    StgBits r;
-                    stg_init(r, lane, p - b8 - tli);
+                int32_t idx = rec_index(rec, hi - p);
+                if (idx < 0 && p > lo) {  // walk the true path until it meets a recorded start
+                    HufRd r;
+                    rd_init(r, lane, p - b8 - tli);
                     do {
-                        const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
-                        p -= (int32_t)(e >> 8);
+                        rd_refill(r, lane, tli);
+                        const uint32_t nb = rd_nbits(r, tmask);
+                        r.u -= (int32_t)nb;
+                        p -= (int32_t)nb;
                         w++;
-                    } while (p > lo && !(synced = recorded(p)));
+                    } while (p > lo && (idx = rec_index(rec, hi - p)) < 0);
                 }
-                if (synced) {
-                    const int32_t d = hi - p;
-                    // boundaries recorded below d (d < 128 here)
-                    const uint64_t m0 = d >= 64 ? ~0ull : ((1ull << d) - 1ull);
-                    const uint64_t m1 = d <= 64 ? 0ull : ((1ull << (d - 64)) - 1ull);
-                    const uint32_t idx = (uint32_t)__builtin_popcountll(bm0 & m0) + (uint32_t)__builtin_popcountll(bm1 & m1);
-                    cnt = w + c - idx;
+                if (idx >= 0) {
+                    cnt = w + c - (uint32_t)idx;
                     ex = q;
                 } else {
                     cnt = w;
@@ -258,33 +276,34 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         // ---- pass B: decode again from the true entry, storing the symbols
         {
             uint8_t* out = sdst + produced + (incl - cnt);
-            int32_t p = entry;
-            StgBits r;
-            stg_init(r, lane, p - b8 - tli);
-            // Lanes that are done keep decoding at their fixed position (their reader stays valid: a
-            // fixed position refills at most once) and store nothing; the trip counts are wave-uniform,
-            // so the loops have no divergent region and the loop-carried state needs no copies.
+            HufRd r;
+            rd_init(r, lane, entry - b8 - tli);
+            // Lanes that are done keep their position (their codeword lengths count as 0) and store
+            // nothing; the trip counts are wave-uniform, so the loops have no divergent region.
             const uint32_t my4 = cnt >> 2, myTail = cnt & 3u;
             const uint32_t n4 = wave_max(my4), nTail = wave_max(myTail);
             for (uint32_t g = 0; g < n4; g++) {
                 P.count(7);
                 const bool act = g < my4;
-                uint32_t word = 0;
+                const uint32_t w8 = act ? 8u : 0u;  // nbBits field width: 0 keeps a finished lane in place
+                uint32_t e[4];
 #pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    uint32_t e1, e2;
-                    stg_entry2(r, lane, p - b8 - tli, tmask, tli, e1, e2);
-                    p -= act ? (int32_t)(e1 >> 8) + (int32_t)(e2 >> 8) : 0;
-                    word |= ((e1 & 0xFFu) | ((e2 & 0xFFu) << 8)) << (16 * u);
+                for (int v = 0; v < 4; v++) {
+                    if ((v & 1) == 0) rd_refill(r, lane, tli);
+                    e[v] = rd_entry(r, tmask);
+                    r.u -= (int32_t)__builtin_amdgcn_ubfe(e[v], 8u, w8);
                 }
+                const uint32_t word = __builtin_amdgcn_perm(e[1], e[0], 0x0C0C0400u) |
+                                      (__builtin_amdgcn_perm(e[3], e[2], 0x0C0C0400u) << 16);
                 if (act) gst<uint32_t>(out + 4u * g, word);
             }
             out += 4u * my4;
             for (uint32_t g = 0; g < nTail; g++) {
                 P.count(8);
                 const bool act = g < myTail;
-                const uint32_t e = stg_entry(r, lane, p - b8 - tli, tmask);
-                p -= act ? (int32_t)(e >> 8) : 0;
+                rd_refill(r, lane, tli);
+                const uint32_t e = rd_entry(r, tmask);
+                r.u -= act ? (int32_t)(e >> 8) : 0;
                 if (act) gst<uint8_t>(out + g, (uint8_t)e);
             }
         }

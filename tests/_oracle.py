@@ -147,6 +147,33 @@ def c5_decompress(blob: bytes, n: int):
     return rc, out[:n]
 
 
+def c5_frames_strictly_valid(blob: bytes) -> bool:
+    """Every zstd frame of a C5 blob decodes under the strict Huffman end rule (each stream ends exactly
+    at its first bit after its symbol count; zstd1_dec.h huf_decode_stream, the rule the GPU decoder
+    follows).  libzstd's double-symbol Huffman decoder (HUF_decompress4X2, picked by a speed
+    heuristic) also accepts a stream followed by one more short codeword, so a corrupted blob can
+    decode under the reference and fail here: tests treat that case as a known divergence."""
+    M = model()
+    p, frames = 0, []
+    for _ in range(4):
+        if p + 8 > len(blob):
+            return True
+        sz = int.from_bytes(blob[p:p + 8], "little")
+        if sz > len(blob) - p - 8:
+            return True
+        frames.append(blob[p + 8:p + 8 + sz])
+        p += 8 + sz
+    frames.append(blob[p:])
+    for f in frames:
+        cs = M.z1m_content_size(_buf(f).ctypes.data, len(f))
+        cap = max(int(cs), 1) if cs >= 0 else 1 << 20
+        out = np.zeros(cap + 64, np.uint8)
+        a = _buf(f)
+        if M.z1m_decompress(a.ctypes.data, len(f), out.ctypes.data, cap) < 0:
+            return False
+    return True
+
+
 def vbz_compress(x: np.ndarray) -> bytes:
     L = oracle()
     x = np.ascontiguousarray(x, dtype=np.int16)
