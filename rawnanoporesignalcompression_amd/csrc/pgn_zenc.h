@@ -1389,7 +1389,8 @@ struct LitOut {
 };
 __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
                                                       PhaseProf& P, uint32_t writeRaw, const uint32_t* prevCw,
-                                                      uint32_t prevCheck, uint32_t* nextCw, uint32_t saveNew)
+                                                      uint32_t prevCheck, uint32_t* nextCw, uint32_t saveNew,
+                                                      uint32_t rawAt)
 {
     EncLds& L = sEnc;
     dst = uni(dst);
@@ -1400,6 +1401,7 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     prevCheck = uni(prevCheck);
     nextCw = uni(nextCw);
     saveNew = uni(saveNew);
+    rawAt = uni(rawAt);  // a section of this size or more makes the block raw: it is then only sized
     auto ret = [](size_t sz, bool nt) { LitOut o; o.size = (uint32_t)sz; o.newTable = nt ? 1u : 0u; return o; };
     auto write_raw_literals_wave = [&](uint8_t* d, const uint8_t* l, uint32_t m) -> size_t {
         if (writeRaw) return pgn::write_raw_literals_wave(d, l, m);
@@ -1556,6 +1558,24 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     for (int q = 0; q < 4; q++) nnz += (uint32_t)__builtin_popcountll(ballot(c[q] != 0));
     const uint32_t hl = huf_tree_wave(maxSym, huffLog, nnz, P);
     P.mark(14);
+    if (!repeat) {
+        // the streams alone already miss the gain the section must make: raw literals whatever the
+        // table description's size (HUF_compress_internal's final check), so it is not written
+        uint32_t b4[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int s = lane + 64 * q;
+            const uint32_t nbq = ((uint32_t)s <= maxSym) ? (uint32_t)L.nbBits[s] : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; k++) b4[k] += seg_count(L, k, s) * nbq;
+        }
+        uint32_t cs = single ? 0u : 6u;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k == 0 || !single) cs += (wave_sum(b4[k]) + 8) >> 3;
+        if (cs >= n - minGain) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
+        if (lhSize + cs >= rawAt) { P.mark(7); return ret(lhSize + cs, false); }
+    }
     hSize = huf_write_ctable_wave(maxSym, hl, P);
     P.count(5);
     P.count(6, maxSym);
@@ -1599,6 +1619,7 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     uint32_t cStreams = single ? bytes[0] : 6 + bytes[0] + bytes[1] + bytes[2] + bytes[3];
     uint32_t total = hSize + cStreams;
     if (total >= n - 1 || total >= n - minGain) { size_t r = write_raw_literals_wave(dst, lit, n); P.mark(7); return ret(r, false); }
+    if (lhSize + total >= rawAt) { P.mark(7); return ret(lhSize + total, false); }
     if (!useOld && saveNew) {  // the table a later block may repeat
 #pragma unroll
         for (int q = 0; q < 4; q++) gst<uint32_t>(nextCw + lane + 64 * q, L.cw[lane + 64 * q]);
@@ -1717,8 +1738,11 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
             uint8_t* body = bdst + 3;
             // without sequences a raw literals section makes the block raw (lh + n + 1 >= maxCSize): it
             // is then only sized here, and the raw block below is the one copy
+            // without sequences the block is compressed only if litSize + 1 < maxCSize
+            const uint32_t maxCSize = bs - ((bs >> 6) + 2);
             const LitOut lo = compress_literals_wave(body, lit, nLit, P, nbSeq > 0 ? 1u : 0u, S.huf + 256 * hufCur, hufCheck,
-                                                     S.huf + 256 * (hufCur ^ 1u), last ? 0u : 1u);
+                                                     S.huf + 256 * (hufCur ^ 1u), last ? 0u : 1u,
+                                                     nbSeq == 0 ? maxCSize - 1u : 0xFFFFFFFFu);
             const size_t litSize = uni(lo.size);
             wave_sync();
             if (nbSeq == 0) {
@@ -1731,7 +1755,6 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
                 seqSize = (r == (size_t)-1 || r == (size_t)-2) ? (size_t)-1 : r;
                 P.mark(8);
             }
-            const size_t maxCSize = bs - ((bs >> 6) + 2);
             if (seqSize != (size_t)-1 && litSize + seqSize < maxCSize) cSize = (uint32_t)(litSize + seqSize);
             // a later block of one repeated byte is an RLE block (never the first: decoders <= 1.4.3)
             if (!first && cSize < 25 && wave_is_rle(src + start, bs)) cSize = 1;
