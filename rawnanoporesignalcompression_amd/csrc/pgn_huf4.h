@@ -39,34 +39,37 @@ __device__ __forceinline__ void hdbg(uint32_t tag, uint32_t a, uint32_t b, uint3
 // bit is at local position u + tl + 32 (row + 1)), nxw is staged word `row` (the next refill).  A
 // refill check every two codewords keeps both peeks inside Wd (u >= tl after it; u < tl + 32 <= 43
 // so u + tl <= 54).  Rows below 0 read the decode table in front of the staging rows: only a path
-// that has left the stream's staged bits does that, and it never uses the bits.
+// that has left the stream's staged bits does that (the rows in front of the staging are LDS of
+// the same workgroup), and it never uses the bits.
 struct HufRd {
     uint64_t Wd;
     int32_t u;
     int32_t row;
     uint32_t nxw;
 };
-__device__ __forceinline__ uint32_t stg_word(int32_t row, int lane)
+// Staging rows: row r of lane l at stg[64 r + l] (word-major, so the lanes of a row hit distinct
+// banks).  The 16-lanes-per-stream decoder uses sDec.stg; the cooperative one (64 lanes per stream,
+// one wave per stream) gives each wave its own rows (sCoopStg).
+__device__ __forceinline__ uint32_t stg_word(const uint32_t* stg, int32_t row, int lane)
 {
-    constexpr int32_t kStgFirst = (int32_t)(__builtin_offsetof(DecLds, stg) / 4);
-    return reinterpret_cast<const uint32_t*>(&sDec)[kStgFirst + 64 * row + lane];
+    return stg[64 * row + lane];
 }
-__device__ __forceinline__ void rd_init(HufRd& r, int lane, int32_t x)  // x = q - b8 - tl
+__device__ __forceinline__ void rd_init(HufRd& r, const uint32_t* stg, int lane, int32_t x)  // x = q - b8 - tl
 {
     int32_t wi = x >> 5;
     wi = wi < 0 ? 0 : (wi > kStgWords - 2 ? kStgWords - 2 : wi);
-    r.Wd = (uint64_t)sDec.stg[wi][lane] | ((uint64_t)sDec.stg[wi + 1][lane] << 32);
+    r.Wd = (uint64_t)stg_word(stg, wi, lane) | ((uint64_t)stg_word(stg, wi + 1, lane) << 32);
     r.u = x - 32 * wi;
     r.row = wi - 1;
-    r.nxw = stg_word(r.row, lane);
+    r.nxw = stg_word(stg, r.row, lane);
 }
-__device__ __forceinline__ void rd_refill(HufRd& r, int lane, int32_t tl)
+__device__ __forceinline__ void rd_refill(HufRd& r, const uint32_t* stg, int lane, int32_t tl)
 {
     const bool rf = r.u < tl;
     r.Wd = rf ? ((r.Wd << 32) | r.nxw) : r.Wd;
     r.u += rf ? 32 : 0;
     r.row -= rf ? 1 : 0;
-    r.nxw = stg_word(r.row, lane);
+    r.nxw = stg_word(stg, r.row, lane);
 }
 // decode-table entry (symbol | nbBits << 8) of the next codeword
 __device__ __forceinline__ uint32_t rd_entry(const HufRd& r, uint32_t tmask)
@@ -79,6 +82,14 @@ __device__ __forceinline__ uint32_t rd_nbits(const HufRd& r, uint32_t tmask)
 }
 // z = u + 32 row: the next codeword's top position is z + (tl + b8 + 32)
 __device__ __forceinline__ int32_t rd_z(const HufRd& r) { return r.u + 32 * r.row; }
+
+// the value of lane j - 1 of the same stream (lane 0 of a stream reads a value it does not use)
+template <int LPS>
+__device__ __forceinline__ int32_t prev_lane(int32_t x)
+{
+    if (LPS == 16) return (int32_t)dpp<kDppRowShr1>((uint32_t)x);
+    return __shfl_up(x, 1, 64);
+}
 
 // Recorded codeword starts: the first kRecSyms starts at or below a lane's window top, as distances
 // below the top, one byte each (0xFF = none; a distance is at most tl - 1 + 19 * 11 < 255).
@@ -103,10 +114,20 @@ __device__ __forceinline__ int32_t rec_index(const RecStarts& R, int32_t d)
 
 // Returns false on a malformed section.  jt = the jump table's three stream sizes (l1 | l2 << 16,
 // l3), read by the caller (remain >= 6).
-__device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                              uint32_t jt01, uint32_t jt2, PhaseProf& P)
+//
+// LPS = lanes per stream: 16 (one wave decodes the four streams, huf_decode4_wave) or 64 (the
+// cooperative decoder: wave kStream decodes stream kStream with all its lanes, wid = its staging).
+constexpr int kCoopWaves = 4;
+// two spare rows in front of each wave's rows (a refill reads at most two rows below row 0)
+static __shared__ uint32_t sCoopStg[kCoopWaves][(kStgWords + 2) * 64];
+
+template <int LPS>
+__device__ __forceinline__ bool huf_decode_lanes(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
+                                                 uint32_t jt01, uint32_t jt2, int kStream, PhaseProf& P)
 {
+    static_assert(LPS == 16 || LPS == 64, "16 or 64 lanes per stream");
     const int lane = lane_id();
+    uint32_t* stg = LPS == 16 ? &sDec.stg[0][0] : &sCoopStg[kStream][2 * 64];
     tl = uni(tl);
     hp = uni(hp);
     remain = uni((uint64_t)remain);
@@ -114,7 +135,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     rs = uni(rs);
     jt01 = uni(jt01);
     jt2 = uni(jt2);
-    const int k = lane >> 4, j = lane & 15;
+    const int k = LPS == 16 ? lane >> 4 : kStream, j = LPS == 16 ? lane & 15 : lane;
     const size_t l1 = jt01 & 0xFFFFu, l2 = jt01 >> 16, l3 = jt2;
     if (l1 + l2 + l3 + 6 > remain) return false;
     const size_t l4 = remain - 6 - l1 - l2 - l3;
@@ -146,12 +167,12 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         const int32_t b8 = 8 * base;
 #pragma unroll
         for (int i = 0; i < kStgWords / 4; i++) {
-            sDec.stg[4 * i][lane] = nx[i].x;
-            sDec.stg[4 * i + 1][lane] = nx[i].y;
-            sDec.stg[4 * i + 2][lane] = nx[i].z;
-            sDec.stg[4 * i + 3][lane] = nx[i].w;
+            stg[64 * (4 * i) + lane] = nx[i].x;
+            stg[64 * (4 * i + 1) + lane] = nx[i].y;
+            stg[64 * (4 * i + 2) + lane] = nx[i].z;
+            stg[64 * (4 * i + 3) + lane] = nx[i].w;
         }
-        const int32_t nextT = T - 16 * kWinBits;
+        const int32_t nextT = T - LPS * kWinBits;
         if (ballot(nextT > 0)) {  // next round's bytes, in flight during this one
             base = round_base(nextT - j * kWinBits);
             round_load(nx, src, sl, base);
@@ -170,10 +191,10 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         int32_t q;
         {
             HufRd r;
-            rd_init(r, lane, ((j == 0 || hi <= lo) ? hi : hi + kOvBits) - b8 - tli);
+            rd_init(r, stg, lane, ((j == 0 || hi <= lo) ? hi : hi + kOvBits) - b8 - tli);
             while (ballot(rd_z(r) > zHi)) {  // overlap: decoded, neither counted nor recorded
                 P.count(1);
-                rd_refill(r, lane, tli);
+                rd_refill(r, stg, lane, tli);
 #pragma unroll
                 for (int v = 0; v < 2; v++) {
                     const uint32_t nb = rd_nbits(r, tmask);
@@ -183,7 +204,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             P.count(2);
 #pragma unroll
             for (int i = 0; i < kRecSyms; i++) {  // the first kRecSyms codewords: recorded and counted
-                if ((i & 1) == 0) rd_refill(r, lane, tli);
+                if ((i & 1) == 0) rd_refill(r, stg, lane, tli);
                 const int32_t z = rd_z(r);
                 const bool act = z > zLo;
                 const uint32_t d = act ? (uint32_t)(zHi - z) : 0xFFu;
@@ -198,7 +219,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 const bool act = rd_z(r) > zLo;
 #pragma unroll
                 for (int v = 0; v < 4; v++) {
-                    if ((v & 1) == 0) rd_refill(r, lane, tli);
+                    if ((v & 1) == 0) rd_refill(r, stg, lane, tli);
                     const uint32_t nb = rd_nbits(r, tmask);
                     r.u -= act ? (int32_t)nb : 0;
                 }
@@ -206,7 +227,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             }
             while (ballot(rd_z(r) > zLo)) {
                 P.count(4);
-                rd_refill(r, lane, tli);
+                rd_refill(r, stg, lane, tli);
 #pragma unroll
                 for (int v = 0; v < 2; v++) {
                     const bool act = rd_z(r) > zLo;
@@ -220,12 +241,15 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         P.mark(11);
         // ---- sync: true entries, symbol counts and exits
         // (DPP reads a disabled source lane as 0: the moves run on the full wave, outside any branch)
-        const int32_t prevQ = (int32_t)dpp<kDppRowShr1>((uint32_t)q);
+        const int32_t prevQ = prev_lane<LPS>(q);
         int32_t entry = (j == 0) ? hi : prevQ;
         uint32_t cnt = c;  // lane 0 starts on the true path
         int32_t ex = q;
-        bool need = j > 0;
-        for (int it = 0; it < 16; it++) {
+        // Only lanes whose window is not empty (hi > 0) take part: the stream's last such lane ends at
+        // its first bit, and the empty ones above it hold no symbols.  Every iteration settles at
+        // least one more lane, so LPS iterations always converge.
+        bool need = j > 0 && hi > 0;
+        for (int it = 0; it < LPS; it++) {
             P.count(5);
             if (need) {
                 int32_t p = entry;
@@ -233,9 +257,9 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 int32_t idx = rec_index(rec, hi - p);
                 if (idx < 0 && p > lo) {  // walk the true path until it meets a recorded start
                     HufRd r;
-                    rd_init(r, lane, p - b8 - tli);
+                    rd_init(r, stg, lane, p - b8 - tli);
                     do {
-                        rd_refill(r, lane, tli);
+                        rd_refill(r, stg, lane, tli);
                         const uint32_t nb = rd_nbits(r, tmask);
                         r.u -= (int32_t)nb;
                         p -= (int32_t)nb;
@@ -253,21 +277,35 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
 #ifdef PGN_PROFILE
             P.count(6, wave_max(need ? cnt : 0u) > 0 ? 1u : 0u);  // sync iterations with any walking lane
 #endif
-            const int32_t prevEx = (int32_t)dpp<kDppRowShr1>((uint32_t)ex);
+            const int32_t prevEx = prev_lane<LPS>(ex);
             const int32_t ne = (j == 0) ? hi : prevEx;
-            need = (j > 0) && (ne != entry);
+            need = (j > 0) && hi > 0 && (ne != entry);
             entry = ne;
             if (!ballot(need)) break;
         }
         P.mark(12);
         // ---- output offsets: DPP prefix over the stream's 16 lanes (one row)
         uint32_t incl = cnt;
-        incl += dpp<kDppRowShr1>(incl);
-        incl += dpp<kDppRowShr2>(incl);
-        incl += dpp<kDppRowShr4>(incl);
-        incl += dpp<kDppRowShr8>(incl);
-        const uint32_t tot = (uint32_t)__shfl((int)incl, lane | 15, 64);
-        const int32_t Tn = __shfl(ex, lane | 15, 64);
+        uint32_t tot;
+        int32_t Tn;
+        const uint64_t live = ballot(hi > 0);  // lanes with a window (contiguous from j = 0 in each stream)
+        if (LPS == 16) {
+            incl += dpp<kDppRowShr1>(incl);
+            incl += dpp<kDppRowShr2>(incl);
+            incl += dpp<kDppRowShr4>(incl);
+            incl += dpp<kDppRowShr8>(incl);
+            tot = (uint32_t)__shfl((int)incl, lane | 15, 64);
+            const uint32_t rowLive = (uint32_t)(live >> (16 * k)) & 0xFFFFu;
+            const int jl = rowLive ? 31 - __builtin_clz(rowLive) : 0;
+            const int32_t exl = __shfl(ex, 16 * k + jl, 64);
+            Tn = rowLive ? exl : T;  // a finished stream stays where it ended
+        } else {
+            incl = wave_incl_sum(incl);
+            tot = readlane_u32(incl, 63);
+            const int jl = live ? 63 - __builtin_clzll(live) : 0;
+            const int32_t exl = (int32_t)__builtin_amdgcn_readlane((int)ex, jl);
+            Tn = live ? exl : T;
+        }
 #ifdef PGN_DEBUG_HUF
         if (produced < 2000) hdbg(2 + 16 * k + 256 * j, (uint32_t)T, (uint32_t)hi, (uint32_t)lo, c, (uint32_t)q,
                                   (uint32_t)entry, cnt | ((uint32_t)ex << 16));
@@ -277,7 +315,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
         {
             uint8_t* out = sdst + produced + (incl - cnt);
             HufRd r;
-            rd_init(r, lane, entry - b8 - tli);
+            rd_init(r, stg, lane, entry - b8 - tli);
             // Lanes that are done keep their position (their codeword lengths count as 0) and store
             // nothing; the trip counts are wave-uniform, so the loops have no divergent region.
             const uint32_t my4 = cnt >> 2, myTail = cnt & 3u;
@@ -289,7 +327,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
                 uint32_t e[4];
 #pragma unroll
                 for (int v = 0; v < 4; v++) {
-                    if ((v & 1) == 0) rd_refill(r, lane, tli);
+                    if ((v & 1) == 0) rd_refill(r, stg, lane, tli);
                     e[v] = rd_entry(r, tmask);
                     r.u -= (int32_t)__builtin_amdgcn_ubfe(e[v], 8u, w8);
                 }
@@ -301,7 +339,7 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
             for (uint32_t g = 0; g < nTail; g++) {
                 P.count(8);
                 const bool act = g < myTail;
-                rd_refill(r, lane, tli);
+                rd_refill(r, stg, lane, tli);
                 const uint32_t e = rd_entry(r, tmask);
                 r.u -= act ? (int32_t)(e >> 8) : 0;
                 if (act) gst<uint8_t>(out + g, (uint8_t)e);
@@ -317,6 +355,18 @@ __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, si
     hdbg(3, (uint32_t)k, (uint32_t)j, (uint32_t)T, produced, nsym, 0, 0);
 #endif
     return !ballot(T != 0 || produced != nsym);
+}
+
+__device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
+                                              uint32_t jt01, uint32_t jt2, PhaseProf& P)
+{
+    return huf_decode_lanes<16>(tl, hp, remain, dst, rs, jt01, jt2, 0, P);
+}
+// one stream of the section with all 64 lanes (cooperative decoder: wave kStream of the workgroup)
+__device__ __noinline__ bool huf_decode1of4_wave64(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
+                                                   uint32_t jt01, uint32_t jt2, int kStream, PhaseProf& P)
+{
+    return huf_decode_lanes<64>(tl, hp, remain, dst, rs, jt01, jt2, kStream, P);
 }
 
 }  // namespace pgn

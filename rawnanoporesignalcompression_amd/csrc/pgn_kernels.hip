@@ -467,6 +467,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     P.flush();
 }
 
+// Small batches (the per-chunk calls): one workgroup of kCoopWaves waves per work unit.  Wave 0
+// decodes the frame; the four Huffman streams of each literals section are decoded by the four
+// waves at once, 64 lanes per stream (pgn_zdec.h CoopCmd).  A lone 100,000-sample chunk's decode
+// is bound by its largest frame's Huffman rounds, which this cuts about fourfold.
+constexpr size_t kCoopMaxChunks = 64;  // batches up to this many chunks use it
+__global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs a)
+{
+    const int lane = lane_id();
+    const int wid = (int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const size_t G = a.G;
+    const uint32_t u = blockIdx.x;
+    if ((size_t)u >= (size_t)a.nu * G) return;
+    const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
+    const size_t g = u % G;
+    const size_t c = a.base + g;
+    if (c >= a.nchunks || a.status[c] != PGN_OK) return;  // the same for every wave of the group
+    PhaseProf P;
+    P.init(a.prof);
+    if (wid != 0) {
+        coop_helper_wave(wid, P);
+        P.flush();
+        return;
+    }
+    const DecLayout lay = dec_layout();
+    uint8_t* sbase = a.slotScratch + (size_t)u * a.slotBytes;
+    DecScratch S;
+    S.lit = sbase + lay.lit;
+    S.seqs = (uint32_t*)(sbase + lay.seqs);
+    S.maxSeq = kMaxDecSeq;
+    S.tables = (uint32_t*)(sbase + lay.tables);
+    S.htab = (uint16_t*)(sbase + lay.htab);
+    S.seg = sbase + lay.seg;
+    S.segCap = 0;
+    S.segDiag = 0;
+    DecUnit& d = a.units[g * kStreams + s];
+    const size_t cap = a.nu == 1 ? (size_t)d.cs + kVbzPadding : (size_t)d.cs;
+    const long r = zstd_decompress_wave<true>(a.in + d.src, d.len, a.inter + g * kChunkInterBytes + d.interOff, cap, S, P);
+    if (lane == 0) d.dres = (int32_t)r;
+    coop_finish();
+    P.flush();
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void dec_merge_kernel(DecArgs a)
 {
     const size_t g = blockIdx.x;
@@ -1683,7 +1725,9 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         if (p >= 2) HIPCHK(hipStreamWaitEvent(s, c->evFree[b], 0));
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         else hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+        if (G <= kCoopMaxChunks && (size_t)nu * G <= slots && !c->hufSegCap)  // few chunks: a workgroup per frame
+            hipLaunchKernelGGL(dec_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopWaves), 0, s, a);
+        else hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
         if (passes > 1) {
             HIPCHK(hipEventRecord(c->evStage[b], s));
             HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));

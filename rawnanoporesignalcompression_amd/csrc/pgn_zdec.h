@@ -864,9 +864,75 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
     return (long)op;
 }
 
-// ZSTD_decompress(dst, dstCap, src, srcSize).  Returns size or a negative z1::DecErr.
+// Cooperative decode (small batches, dec_zstd_coop_kernel): a workgroup of kCoopWaves waves per
+// frame.  Wave 0 runs zstd_decompress_wave<true>; at a four-stream Huffman section it posts the
+// section here and the four waves decode one stream each with 64 lanes (huf_decode1of4_wave64);
+// everything else is wave 0's.  The other waves wait in coop_helper_wave.
+struct CoopCmd {
+    const uint8_t* hp;
+    uint8_t* dst;
+    uint64_t remain;
+    uint32_t rs, jt01, jt2, tl;
+    uint32_t done;  // no more sections: the helpers leave
+    uint32_t bad;   // a helper's stream failed
+};
+static __shared__ CoopCmd sCoop;
+
+__device__ __noinline__ void coop_helper_wave(int wid, PhaseProf& P)
+{
+#ifdef PGN_COOP_DIAG
+    return;
+#endif
+    while (true) {
+        __syncthreads();  // B1: a section (or done) is posted
+        if (sCoop.done) break;
+        const bool ok = huf_decode1of4_wave64(sCoop.tl, sCoop.hp, sCoop.remain, sCoop.dst, sCoop.rs, sCoop.jt01,
+                                              sCoop.jt2, wid, P);
+        if (!ok && lane_id() == 0) sCoop.bad = 1;
+        __syncthreads();  // B2: every stream of the section is decoded
+    }
+}
+// wave 0's side of one section
+__device__ __forceinline__ bool coop_section(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
+                                             uint32_t jt01, uint32_t jt2, PhaseProf& P)
+{
+    if (lane_id() == 0) {
+        sCoop.hp = hp;
+        sCoop.dst = dst;
+        sCoop.remain = remain;
+        sCoop.rs = rs;
+        sCoop.jt01 = jt01;
+        sCoop.jt2 = jt2;
+        sCoop.tl = tl;
+        sCoop.done = 0;
+        sCoop.bad = 0;
+    }
+#ifdef PGN_COOP_DIAG  // diagnostic: wave 0 decodes the four streams one after another, no helpers
+    bool ok = true;
+    for (int k = 0; k < 4; k++) ok = huf_decode1of4_wave64(tl, hp, remain, dst, rs, jt01, jt2, k, P) && ok;
+    return ok;
+#else
+    __syncthreads();  // B1
+    const bool ok = huf_decode1of4_wave64(tl, hp, remain, dst, rs, jt01, jt2, 0, P);
+    __syncthreads();  // B2
+    return ok && sCoop.bad == 0;
+#endif
+}
+// wave 0 releases the helpers after its frame
+__device__ __forceinline__ void coop_finish()
+{
+#ifdef PGN_COOP_DIAG
+    return;
+#endif
+    if (lane_id() == 0) sCoop.done = 1;
+    __syncthreads();  // B1 with done set
+}
+
+// ZSTD_decompress(dst, dstCap, src, srcSize).  Returns size or a negative z1::DecErr.  COOP: wave 0
+// of a dec_zstd_coop_kernel workgroup (four-stream Huffman sections shared with the other waves).
+template <bool COOP = false>
 __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ src, size_t srcSize, uint8_t* __restrict__ dst,
-                                            size_t dstCap, DecScratch S, PhaseProf& P)
+                                                  size_t dstCap, DecScratch S, PhaseProf& P)
 {
     const int lane = lane_id();
     src = uni(src);
@@ -1022,7 +1088,9 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                             const size_t jp = (size_t)(hp - src);  // the jump table, from the header window
                             const uint32_t jt01 = hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16);
                             const uint32_t jt2 = hw_u16(hw, src, jp + 4);
-                            if (S.segCap)
+                            if (COOP)
+                                ok = coop_section(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, P);
+                            else if (S.segCap)
                                 ok = huf_seg_decode4_wave(hufTl, hufMinNb, hp, remain, litOut, (uint32_t)rs, jt01, jt2,
                                                           S.seg, S.segCap, P, S.segDiag);
                             else
