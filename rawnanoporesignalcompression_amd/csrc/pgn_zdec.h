@@ -880,9 +880,6 @@ static __shared__ CoopCmd sCoop;
 
 __device__ __noinline__ void coop_helper_wave(int wid, PhaseProf& P)
 {
-#ifdef PGN_COOP_DIAG
-    return;
-#endif
     while (true) {
         __syncthreads();  // B1: a section (or done) is posted
         if (sCoop.done) break;
@@ -907,23 +904,14 @@ __device__ __forceinline__ bool coop_section(unsigned tl, const uint8_t* hp, siz
         sCoop.done = 0;
         sCoop.bad = 0;
     }
-#ifdef PGN_COOP_DIAG  // diagnostic: wave 0 decodes the four streams one after another, no helpers
-    bool ok = true;
-    for (int k = 0; k < 4; k++) ok = huf_decode1of4_wave64(tl, hp, remain, dst, rs, jt01, jt2, k, P) && ok;
-    return ok;
-#else
     __syncthreads();  // B1
     const bool ok = huf_decode1of4_wave64(tl, hp, remain, dst, rs, jt01, jt2, 0, P);
     __syncthreads();  // B2
     return ok && sCoop.bad == 0;
-#endif
 }
 // wave 0 releases the helpers after its frame
 __device__ __forceinline__ void coop_finish()
 {
-#ifdef PGN_COOP_DIAG
-    return;
-#endif
     if (lane_id() == 0) sCoop.done = 1;
     __syncthreads();  // B1 with done set
 }
