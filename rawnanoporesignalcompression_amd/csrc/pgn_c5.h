@@ -394,17 +394,41 @@ __device__ inline void c5_split_counts(const int16_t* __restrict__ x, uint32_t n
     using CO = ClassOffsets<C4>;
     const uint32_t lane = (uint32_t)lane_id();
     uint32_t s = 0, m = 0, l = 0;
-    for (uint32_t t = t0 + 16u * lane; t < t1; t += 1024u) {
-        uint32_t prev = t ? (uint32_t)gld<uint16_t>(x + t - 1) : 0u;
-        const uint32_t e = t + 16u < t1 ? t + 16u : t1;
-        for (uint32_t i = t; i < e; i++) {
-            const uint32_t v = gld<uint16_t>(x + i);
-            const uint32_t d = (v - prev) & 0xFFFFu;
-            const uint32_t z = ((d << 1) ^ (0u - (d >> 15))) & 0xFFFFu;
-            prev = v;
-            s += (z >= 1u && z <= CO::t1) ? 1u : 0u;
-            m += (z > CO::t1 && z <= CO::t2) ? 1u : 0u;
-            l += (z > CO::t2) ? 1u : 0u;
+    // four 1,024-sample steps per trip, their loads issued together (the pass is latency-bound)
+    for (uint32_t tb = t0; tb < t1; tb += 4096u) {
+        uint32_t wv[4][8], pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + 1024u * u + 16u * lane;
+            pv[u] = (t < t1 && t) ? (uint32_t)gld<uint16_t>(x + t - 1) : 0u;
+            if (t + 16u <= t1) {
+                const uint4 a = gld<uint4>(x + t), b = gld<uint4>(x + t + 8);
+                wv[u][0] = a.x; wv[u][1] = a.y; wv[u][2] = a.z; wv[u][3] = a.w;
+                wv[u][4] = b.x; wv[u][5] = b.y; wv[u][6] = b.z; wv[u][7] = b.w;
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < 8; k++) {
+                    const uint32_t lo = t + 2 * k < t1 ? (uint32_t)gld<uint16_t>(x + t + 2 * k) : 0u;
+                    const uint32_t hi = t + 2 * k + 1 < t1 ? (uint32_t)gld<uint16_t>(x + t + 2 * k + 1) : 0u;
+                    wv[u][k] = lo | (hi << 16);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + 1024u * u + 16u * lane;
+            uint32_t prev = pv[u];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; k++) {
+                const bool in = t + k < t1;
+                const uint32_t v = (wv[u][k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint32_t d = (v - prev) & 0xFFFFu;
+                const uint32_t z = ((d << 1) ^ (0u - (d >> 15))) & 0xFFFFu;
+                prev = v;
+                s += (in && z >= 1u && z <= CO::t1) ? 1u : 0u;
+                m += (in && z > CO::t1 && z <= CO::t2) ? 1u : 0u;
+                l += (in && z > CO::t2) ? 1u : 0u;
+            }
         }
     }
     cS = wave_sum(s);
@@ -705,8 +729,15 @@ __device__ inline uint32_t c5_range_delta_sum(const uint8_t* __restrict__ in, ui
     // S: bytes [s0 / 2, (s1 + 1) / 2), nibble i of the range in byte i / 2
     {
         const uint64_t b0 = ps + (s0 >> 1), b1 = ps + ((s1 + 1) >> 1);
-        for (uint64_t blk = (b0 & ~(uint64_t)15) + 16u * lane; blk < b1; blk += 1024) {
-            const uint4 v = gld<uint4>(in + blk);
+        for (uint64_t bb = (b0 & ~(uint64_t)15) + 16u * lane; bb < b1; bb += 4096) {
+          uint4 vv[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) vv[u] = bb + 1024u * u < b1 ? gld<uint4>(in + bb + 1024u * u) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            const uint64_t blk = bb + 1024u * u;
+            if (blk >= b1) break;
+            const uint4 v = vv[u];
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 16; j++) {
@@ -715,17 +746,24 @@ __device__ inline uint32_t c5_range_delta_sum(const uint8_t* __restrict__ in, ui
                 if (nib0 >= s0 && nib0 < s1) acc += zz_dec16((uint16_t)((by & 15u) + CO::o1));
                 if (nib0 + 1 >= s0 && nib0 + 1 < s1) acc += zz_dec16((uint16_t)((by >> 4) + CO::o1));
             }
+          }
         }
     }
     {
         const uint64_t b0 = pm + m0, b1 = pm + m1;
-        for (uint64_t blk = (b0 & ~(uint64_t)15) + 16u * lane; blk < b1; blk += 1024) {
-            const uint4 v = gld<uint4>(in + blk);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (uint64_t bb = (b0 & ~(uint64_t)15) + 16u * lane; bb < b1; bb += 4096) {
+            uint4 vv[4];
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const uint64_t p = blk + j;
-                if (p >= b0 && p < b1) acc += zz_dec16((uint16_t)(((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) + CO::o2));
+            for (int u = 0; u < 4; u++) vv[u] = bb + 1024u * u < b1 ? gld<uint4>(in + bb + 1024u * u) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint64_t blk = bb + 1024u * u;
+                const uint32_t w[4] = {vv[u].x, vv[u].y, vv[u].z, vv[u].w};
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const uint64_t p = blk + j;
+                    if (p >= b0 && p < b1) acc += zz_dec16((uint16_t)(((w[j >> 2] >> (8 * (j & 3))) & 0xFFu) + CO::o2));
+                }
             }
         }
     }
@@ -741,20 +779,33 @@ __device__ inline void c5_class_counts(const uint8_t* __restrict__ in, uint32_t 
 {
     const uint32_t lane = (uint32_t)lane_id();
     uint32_t s = 0, m = 0, l = 0;
-    for (uint32_t t = t0 + 16u * lane; t < t1; t += 1024u) {
-        const uint32_t nK = (n - t + 3) / 4 < 4u ? (n - t + 3) / 4 : 4u;
-        uint32_t kw = 0;
-        if (nK == 4) {
-            kw = ld32u(in + (t >> 2));
-        } else {
-            for (uint32_t b = 0; b < nK; b++) kw |= (uint32_t)gb(in + (t >> 2) + b) << (8u * b);
+    // four 1,024-sample steps per trip, their key loads issued together
+    for (uint32_t tb = t0; tb < t1; tb += 4096u) {
+        uint32_t kw[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + 1024u * u + 16u * lane;
+            kw[u] = 0;
+            if (t < t1) {
+                const uint32_t nK = (n - t + 3) / 4 < 4u ? (n - t + 3) / 4 : 4u;
+                if (nK == 4) {
+                    kw[u] = ld32u(in + (t >> 2));
+                } else {
+                    for (uint32_t b = 0; b < nK; b++) kw[u] |= (uint32_t)gb(in + (t >> 2) + b) << (8u * b);
+                }
+            }
         }
-        const uint32_t nv = n - t;
-        if (nv < 16) kw &= (1u << (2u * nv)) - 1u;
-        const uint32_t lo = kw & 0x55555555u, hi = (kw >> 1) & 0x55555555u;
-        s += (uint32_t)__builtin_popcount(lo & ~hi);
-        m += (uint32_t)__builtin_popcount(hi & ~lo);
-        l += (uint32_t)__builtin_popcount(lo & hi);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t = tb + 1024u * u + 16u * lane;
+            uint32_t k = kw[u];
+            if (t >= t1) k = 0;
+            else if (n - t < 16) k &= (1u << (2u * (n - t))) - 1u;
+            const uint32_t lo = k & 0x55555555u, hi = (k >> 1) & 0x55555555u;
+            s += (uint32_t)__builtin_popcount(lo & ~hi);
+            m += (uint32_t)__builtin_popcount(hi & ~lo);
+            l += (uint32_t)__builtin_popcount(lo & hi);
+        }
     }
     cS = wave_sum(s);
     cM = wave_sum(m);

@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
 // samples) place each range in the S / M / class-3 streams; the waves split their ranges at once;
 // then the S bytes shared by two ranges (an odd nibble start) and a trailing half byte are written
 // from the nibbles the waves handed over.
-constexpr int kSplitWaves = 16;
+constexpr int kSplitWaves = 8;
 constexpr size_t kSplitWgMaxChunks = 64;  // batches up to this many chunks use it
 __global__ __launch_bounds__(64 * kSplitWaves) void enc_split_wg_kernel(EncArgs a)
 {
