@@ -49,12 +49,15 @@ struct HufRd {
 };
 // Staging rows: row r of lane l at stg[64 r + l] (word-major, so the lanes of a row hit distinct
 // banks).  The 16-lanes-per-stream decoder uses sDec.stg; the cooperative one (64 lanes per stream,
-// one wave per stream) gives each wave its own rows (sCoopStg).
-__device__ __forceinline__ uint32_t stg_word(const uint32_t* stg, int32_t row, int lane)
+// one wave per stream) gives each wave its own rows in its kernel's LDS, passed as an LDS pointer (an
+// LDS variable named by non-kernel functions of several kernels would move the others' LDS behind
+// a per-kernel offset table).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ uint32_t stg_word(const lds_u32* stg, int32_t row, int lane)
 {
     return stg[64 * row + lane];
 }
-__device__ __forceinline__ void rd_init(HufRd& r, const uint32_t* stg, int lane, int32_t x)  // x = q - b8 - tl
+__device__ __forceinline__ void rd_init(HufRd& r, const lds_u32* stg, int lane, int32_t x)  // x = q - b8 - tl
 {
     int32_t wi = x >> 5;
     wi = wi < 0 ? 0 : (wi > kStgWords - 2 ? kStgWords - 2 : wi);
@@ -63,7 +66,7 @@ __device__ __forceinline__ void rd_init(HufRd& r, const uint32_t* stg, int lane,
     r.row = wi - 1;
     r.nxw = stg_word(stg, r.row, lane);
 }
-__device__ __forceinline__ void rd_refill(HufRd& r, const uint32_t* stg, int lane, int32_t tl)
+__device__ __forceinline__ void rd_refill(HufRd& r, const lds_u32* stg, int lane, int32_t tl)
 {
     const bool rf = r.u < tl;
     r.Wd = rf ? ((r.Wd << 32) | r.nxw) : r.Wd;
@@ -116,18 +119,19 @@ __device__ __forceinline__ int32_t rec_index(const RecStarts& R, int32_t d)
 // l3), read by the caller (remain >= 6).
 //
 // LPS = lanes per stream: 16 (one wave decodes the four streams, huf_decode4_wave) or 64 (the
-// cooperative decoder: wave kStream decodes stream kStream with all its lanes, wid = its staging).
+// cooperative decoder: wave kStream decodes stream kStream with all its lanes; coopStg = its rows,
+// with two spare rows in front: a refill reads at most two rows below row 0).
 constexpr int kCoopWaves = 4;
-// two spare rows in front of each wave's rows (a refill reads at most two rows below row 0)
-static __shared__ uint32_t sCoopStg[kCoopWaves][(kStgWords + 2) * 64];
+constexpr int kCoopStgWords = (kStgWords + 2) * 64;  // per wave
 
 template <int LPS>
 __device__ __forceinline__ bool huf_decode_lanes(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                                 uint32_t jt01, uint32_t jt2, int kStream, PhaseProf& P)
+                                                 uint32_t jt01, uint32_t jt2, int kStream, lds_u32* coopStg,
+                                                 PhaseProf& P)
 {
     static_assert(LPS == 16 || LPS == 64, "16 or 64 lanes per stream");
     const int lane = lane_id();
-    uint32_t* stg = LPS == 16 ? &sDec.stg[0][0] : &sCoopStg[kStream][2 * 64];
+    lds_u32* stg = LPS == 16 ? (lds_u32*)&sDec.stg[0][0] : coopStg;
     tl = uni(tl);
     hp = uni(hp);
     remain = uni((uint64_t)remain);
@@ -360,13 +364,14 @@ __device__ __forceinline__ bool huf_decode_lanes(unsigned tl, const uint8_t* hp,
 __device__ __noinline__ bool huf_decode4_wave(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
                                               uint32_t jt01, uint32_t jt2, PhaseProf& P)
 {
-    return huf_decode_lanes<16>(tl, hp, remain, dst, rs, jt01, jt2, 0, P);
+    return huf_decode_lanes<16>(tl, hp, remain, dst, rs, jt01, jt2, 0, nullptr, P);
 }
-// one stream of the section with all 64 lanes (cooperative decoder: wave kStream of the workgroup)
+// one stream of the section with all 64 lanes (cooperative decoder: wave kStream of the workgroup,
+// stg = its staging rows)
 __device__ __noinline__ bool huf_decode1of4_wave64(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                                   uint32_t jt01, uint32_t jt2, int kStream, PhaseProf& P)
+                                                   uint32_t jt01, uint32_t jt2, int kStream, lds_u32* stg, PhaseProf& P)
 {
-    return huf_decode_lanes<64>(tl, hp, remain, dst, rs, jt01, jt2, kStream, P);
+    return huf_decode_lanes<64>(tl, hp, remain, dst, rs, jt01, jt2, kStream, stg, P);
 }
 
 }  // namespace pgn

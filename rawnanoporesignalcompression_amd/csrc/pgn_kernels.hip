@@ -442,6 +442,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
     S.seg = sbase + lay.seg;
+    S.coopCmd = nullptr;
+    S.coopStg = nullptr;
     S.segCap = a.segCap;
     S.segDiag = a.segDiag;
     PhaseProf P;
@@ -485,8 +487,12 @@ __global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs 
     if (c >= a.nchunks || a.status[c] != PGN_OK) return;  // the same for every wave of the group
     PhaseProf P;
     P.init(a.prof);
+    __shared__ uint32_t stgAll[kCoopWaves * kCoopStgWords];
+    __shared__ CoopCmd cmdLds;
+    lds_cmd* cmd = (lds_cmd*)&cmdLds;
+    lds_u32* stg = (lds_u32*)&stgAll[wid * kCoopStgWords + 2 * 64];
     if (wid != 0) {
-        coop_helper_wave(wid, P);
+        coop_helper_wave(wid, cmd, stg, P);
         P.flush();
         return;
     }
@@ -499,13 +505,17 @@ __global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs 
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
     S.seg = sbase + lay.seg;
+    S.coopCmd = nullptr;
+    S.coopStg = nullptr;
     S.segCap = 0;
     S.segDiag = 0;
+    S.coopCmd = cmd;
+    S.coopStg = stg;
     DecUnit& d = a.units[g * kStreams + s];
     const size_t cap = a.nu == 1 ? (size_t)d.cs + kVbzPadding : (size_t)d.cs;
     const long r = zstd_decompress_wave<true>(a.in + d.src, d.len, a.inter + g * kChunkInterBytes + d.interOff, cap, S, P);
     if (lane == 0) d.dres = (int32_t)r;
-    coop_finish();
+    coop_finish(cmd);
     P.flush();
 }
 
@@ -1033,6 +1043,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
     S.seg = sbase + lay.seg;
+    S.coopCmd = nullptr;
+    S.coopStg = nullptr;
     S.segCap = a.segCap;
     S.segDiag = a.segDiag;
     uint8_t* inter = sbase + lay.bytes;
@@ -1213,6 +1225,7 @@ struct pgn_ctx {
     size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH, staged pipeline)
     uint32_t hufSegCap = 0;  // the one-pass Huffman decoder (PGN_HUF=seg) or the two-pass one (0, default)
     uint32_t segDiag = 0;    // PGN_SEG_DIAG: timing experiments on the one-pass decoder (wrong output)
+    bool diagNoMerge = false;  // PGN_DIAG_NO_MERGE: decode without the merge kernel (timing only, wrong output)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
@@ -1345,6 +1358,7 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     }
     if (const char* pp = getenv("PGN_DEC_PIPELINE")) c->decStaged = strcmp(pp, "staged") == 0;
     if (const char* dg = getenv("PGN_SEG_DIAG")) c->segDiag = (uint32_t)atoi(dg);
+    if (const char* nm = getenv("PGN_DIAG_NO_MERGE")) c->diagNoMerge = atoi(nm) != 0;
     if (const char* h = getenv("PGN_HUF")) c->hufSegCap = strcmp(h, "seg") == 0 ? (uint32_t)kSegScratch : 0u;
     if (const char* sb = getenv("PGN_SUBBATCH")) {
         long v = atol(sb);
@@ -1732,7 +1746,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
             HIPCHK(hipEventRecord(c->evStage[b], s));
             HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
         }
-        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        if (c->diagNoMerge) {
+        } else if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         else if (G <= kMergeWgMaxChunks)  // few chunks: one workgroup of kMergeWaves waves per chunk
             hipLaunchKernelGGL(dec_merge_wg_kernel, dim3((unsigned)G), dim3(64 * kMergeWaves), 0, sideS, a);
         else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);

@@ -6,6 +6,15 @@
 
 namespace pgn {
 
+// The encoder's and the decoder's wave workspaces (EncLds in pgn_zenc.h, DecLds in pgn_zdec.h) are
+// one LDS variable.  Two variables named by non-kernel functions of different kernel sets make LLVM's
+// LDS lowering keep only one of them at a fixed address and reach the other through a per-kernel
+// offset table (a scalar load on its access paths; which one depends on how many kernels reach
+// each, so adding a decode kernel moved the encoder's behind the table: encode +4 %).  One variable
+// reached by every codec kernel sits at offset 0 in each of them.
+constexpr size_t kCodecLdsBytes = 8192;
+static __shared__ __attribute__((aligned(16))) uint8_t sCodecLds[kCodecLdsBytes];
+
 constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }

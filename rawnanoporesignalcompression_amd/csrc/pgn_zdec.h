@@ -64,7 +64,8 @@ struct SeqState {
 };
 
 // One instance per decode workgroup (namespace scope, so every access is a DS instruction).
-static __shared__ DecLds sDec;
+static_assert(sizeof(DecLds) <= kCodecLdsBytes, "decoder LDS exceeds the codec LDS");
+#define sDec (*reinterpret_cast<DecLds*>(sCodecLds))
 
 struct DecScratch {
     uint8_t* lit;           // literals of a block with sequences (<= 128 KiB)
@@ -75,6 +76,8 @@ struct DecScratch {
     uint8_t* seg;           // segment regions of the one-pass Huffman decoder (pgn_hufseg.h)
     uint32_t segCap;        // their bytes; 0 selects the two-pass decoder (pgn_huf4.h)
     uint32_t segDiag;       // diagnostic switches (PGN_SEG_DIAG, timing experiments only; wrong output)
+    struct CoopCmd __attribute__((address_space(3)))* coopCmd;  // cooperative decode: the section post
+    __attribute__((address_space(3))) uint32_t* coopStg;         // ... and wave 0's staging rows
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -876,43 +879,43 @@ struct CoopCmd {
     uint32_t done;  // no more sections: the helpers leave
     uint32_t bad;   // a helper's stream failed
 };
-static __shared__ CoopCmd sCoop;
+typedef __attribute__((address_space(3))) CoopCmd lds_cmd;
 
-__device__ __noinline__ void coop_helper_wave(int wid, PhaseProf& P)
+__device__ __noinline__ void coop_helper_wave(int wid, lds_cmd* cmd, lds_u32* stg, PhaseProf& P)
 {
     while (true) {
         __syncthreads();  // B1: a section (or done) is posted
-        if (sCoop.done) break;
-        const bool ok = huf_decode1of4_wave64(sCoop.tl, sCoop.hp, sCoop.remain, sCoop.dst, sCoop.rs, sCoop.jt01,
-                                              sCoop.jt2, wid, P);
-        if (!ok && lane_id() == 0) sCoop.bad = 1;
+        if (cmd->done) break;
+        const bool ok = huf_decode1of4_wave64(cmd->tl, cmd->hp, cmd->remain, cmd->dst, cmd->rs, cmd->jt01, cmd->jt2,
+                                              wid, stg, P);
+        if (!ok && lane_id() == 0) cmd->bad = 1;
         __syncthreads();  // B2: every stream of the section is decoded
     }
 }
 // wave 0's side of one section
 __device__ __forceinline__ bool coop_section(unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst, uint32_t rs,
-                                             uint32_t jt01, uint32_t jt2, PhaseProf& P)
+                                             uint32_t jt01, uint32_t jt2, lds_cmd* cmd, lds_u32* stg, PhaseProf& P)
 {
     if (lane_id() == 0) {
-        sCoop.hp = hp;
-        sCoop.dst = dst;
-        sCoop.remain = remain;
-        sCoop.rs = rs;
-        sCoop.jt01 = jt01;
-        sCoop.jt2 = jt2;
-        sCoop.tl = tl;
-        sCoop.done = 0;
-        sCoop.bad = 0;
+        cmd->hp = hp;
+        cmd->dst = dst;
+        cmd->remain = remain;
+        cmd->rs = rs;
+        cmd->jt01 = jt01;
+        cmd->jt2 = jt2;
+        cmd->tl = tl;
+        cmd->done = 0;
+        cmd->bad = 0;
     }
     __syncthreads();  // B1
-    const bool ok = huf_decode1of4_wave64(tl, hp, remain, dst, rs, jt01, jt2, 0, P);
+    const bool ok = huf_decode1of4_wave64(tl, hp, remain, dst, rs, jt01, jt2, 0, stg, P);
     __syncthreads();  // B2
-    return ok && sCoop.bad == 0;
+    return ok && cmd->bad == 0;
 }
 // wave 0 releases the helpers after its frame
-__device__ __forceinline__ void coop_finish()
+__device__ __forceinline__ void coop_finish(lds_cmd* cmd)
 {
-    if (lane_id() == 0) sCoop.done = 1;
+    if (lane_id() == 0) cmd->done = 1;
     __syncthreads();  // B1 with done set
 }
 
@@ -1077,7 +1080,8 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                             const uint32_t jt01 = hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16);
                             const uint32_t jt2 = hw_u16(hw, src, jp + 4);
                             if (COOP)
-                                ok = coop_section(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, P);
+                                ok = coop_section(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, S.coopCmd,
+                                                  S.coopStg, P);
                             else if (S.segCap)
                                 ok = huf_seg_decode4_wave(hufTl, hufMinNb, hp, remain, litOut, (uint32_t)rs, jt01, jt2,
                                                           S.seg, S.segCap, P, S.segDiag);

@@ -88,8 +88,9 @@ __device__ __forceinline__ uint32_t seg_count(const EncLds& L, int k, int s)
     return (L.hist2[k >> 1][s] >> (16 * (k & 1))) & 0xFFFFu;
 }
 
-// One instance per encode workgroup (namespace scope, so every access is a DS instruction).
-static __shared__ EncLds sEnc;
+// One instance per encode workgroup (the shared codec LDS, pgn_wave.h: every access is a DS instruction).
+static_assert(sizeof(EncLds) <= kCodecLdsBytes, "encoder LDS exceeds the codec LDS");
+#define sEnc (*reinterpret_cast<EncLds*>(sCodecLds))
 
 struct EncScratch {
     uint32_t* ht;        // 2^15 hash-table entries: tag << kTagShift | fingerprint of the 4 bytes | index
