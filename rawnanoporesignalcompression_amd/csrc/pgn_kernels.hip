@@ -1238,12 +1238,15 @@ struct pgn_ctx {
     uint8_t* decChunks = nullptr;  // per buffer: G * kChunkInterBytes + units
     size_t decG = 0;
     DecUnit* lastUnits = nullptr;  // decode records of the last pass (diagnostics)
-    uint32_t* queues = nullptr;    // one work counter per sub-batch pass
+    uint32_t* queues = nullptr;    // a ring of work counters, zeroed when it wraps (one per sub-batch pass)
+    size_t qNext = 0;              // next unused counter of the ring
+    uint32_t* qCur = nullptr;      // the current call's counters
     size_t nQueues = 0;
     // host-call staging: a device buffer and its pinned host mirror (same layout), so a per-chunk
     // call is one upload, the launches and one download
     uint8_t* stage = nullptr;
     uint8_t* hstage = nullptr;
+    uint8_t* hstageDev = nullptr;  // the device's address of hstage (kernels write the call's outputs there)
     size_t stageBytes = 0;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // two-stream pipeline over sub-batches (launch_encode / launch_decode): the side stream runs the
@@ -1489,18 +1492,30 @@ static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
     return PGN_OK;
 }
 
+// n fresh zeroed work counters for this call (c->qCur).  The counters come from a ring that is zeroed
+// only when it wraps: a per-call memset was a fill kernel plus a launch gap in front of every
+// per-chunk call.  Launch sequences on a context are ordered (evLast), so the wrap's memset runs
+// after every earlier user of the ring.
 static int ensure_queues(pgn_ctx* c, size_t n, hipStream_t s)
 {
-    if (n > c->nQueues) {
+    constexpr size_t kRing = 1 << 14;
+    if (!c->queues || n > c->nQueues) {
         wait_last_host(c);
         (void)hipStreamSynchronize(s);
         (void)hipFree(c->queues);
         c->queues = nullptr;
-        size_t m = n < 64 ? 64 : n;
+        const size_t m = n < kRing ? kRing : n;
         HIPCHK(hipMalloc(&c->queues, 4 * m));
+        HIPCHK(hipMemsetAsync(c->queues, 0, 4 * m, s));
         c->nQueues = m;
+        c->qNext = 0;
     }
-    HIPCHK(hipMemsetAsync(c->queues, 0, 4 * n, s));
+    if (c->qNext + n > c->nQueues) {
+        HIPCHK(hipMemsetAsync(c->queues, 0, 4 * c->nQueues, s));
+        c->qNext = 0;
+    }
+    c->qCur = c->queues + c->qNext;
+    c->qNext += n;
     return PGN_OK;
 }
 
@@ -1533,7 +1548,7 @@ static int launch_encode_fused(pgn_ctx* c, int codec, size_t nchunks, const int1
     a.slotBytes = enc_slot_bytes();
     a.epochs = c->epochs;
     a.prof = c->prof;
-    a.queue = c->queues;
+    a.queue = c->qCur;
     a.capN = kPassSamples;
     a.list = nullptr;
     return launch_enc_chunks(codec, a, slots, s);
@@ -1577,7 +1592,7 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     a.slotScratch = c->decScratch;
     a.slotBytes = dec_slot_bytes();
     a.prof = c->prof ? c->prof + kPhases : nullptr;
-    a.queue = c->queues;
+    a.queue = c->qCur;
     a.segCap = c->hufSegCap;
     a.segDiag = c->segDiag;
     a.capN = kPassSamples;
@@ -1661,7 +1676,7 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
         a.sizes = (uint32_t*)(a.frames + G * kChunkFrameBytes);
         a.fsizes = a.sizes + G * kStreams;
         a.base = p * G;
-        a.queue = c->queues + p;
+        a.queue = c->qCur + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(c->side, c->evFree[b], 0));
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         else if (G <= kSplitWgMaxChunks)  // few chunks: one workgroup of kSplitWaves waves per chunk
@@ -1735,7 +1750,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         a.units = (DecUnit*)(buf + G * kChunkInterBytes);
         c->lastUnits = a.units;
         a.base = p * G;
-        a.queue = c->queues + p;
+        a.queue = c->qCur + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(s, c->evFree[b], 0));
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         else hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
@@ -2196,6 +2211,7 @@ static int ensure_stage(pgn_ctx* c, size_t bytes)
     size_t b = align_up(bytes, 1 << 20);
     HIPCHK(hipMalloc(&c->stage, b));
     HIPCHK(hipHostMalloc((void**)&c->hstage, b, hipHostMallocDefault));
+    HIPCHK(hipHostGetDevicePointer((void**)&c->hstageDev, c->hstage, 0));
     c->stageBytes = b;
     return PGN_OK;
 }
@@ -2208,8 +2224,8 @@ struct StageHdr {
 };
 
 // One chunk from host memory: header and samples staged in the pinned mirror and uploaded in one
-// copy; the header and the destination area (cap bytes) come back in two queued copies and one
-// wait; the blob leaves the pinned mirror by memcpy.
+// copy; the kernels write the blob, its size, status and stats straight into the pinned mirror
+// (no copies back: the call's tail is the kernels and one wait); the blob leaves it by memcpy.
 static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap,
                            size_t* out_size)
 {
@@ -2222,19 +2238,18 @@ static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t
     if (rc) return rc;
     uint8_t* dh = c->stage;
     uint8_t* din = c->stage + hdrB;
-    uint8_t* dout = din + inB;
+    uint8_t* hout = c->hstageDev + hdrB + inB;  // the blob, written by the kernels into host memory
     StageHdr* hh = (StageHdr*)c->hstage;
+    StageHdr* hd = (StageHdr*)c->hstageDev;     // the same header, the outputs written by the kernels
     *hh = StageHdr{};
     hh->outCap = cap;
     hh->count = (uint32_t)n;
     if (n) memcpy(c->hstage + hdrB, samples, 2 * n);
     HIPCHK(hipMemcpyAsync(dh, c->hstage, hdrB + 2 * n, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
-    rc = launch_encode(c, codec, 1, (const int16_t*)din, &d->off0, &d->count, dout, &d->outOff, &d->outCap,
-                       &d->outSize, &d->status, d->stats, c->stream, n ? (uint32_t)n : 1u);
+    rc = launch_encode(c, codec, 1, (const int16_t*)din, &d->off0, &d->count, hout, &d->outOff, &d->outCap,
+                       &hd->outSize, &hd->status, hd->stats, c->stream, n ? (uint32_t)n : 1u);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(c->hstage, dh, sizeof(StageHdr), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->hstage + hdrB + inB, dout, cap, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     *out_size = (size_t)hh->outSize;
     if (hh->status != PGN_OK) return hh->status;
@@ -2253,19 +2268,18 @@ static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t l
     if (rc) return rc;
     uint8_t* dh = c->stage;
     uint8_t* din = c->stage + hdrB;
-    int16_t* dout = (int16_t*)(din + inB);
+    int16_t* hout = (int16_t*)(c->hstageDev + hdrB + inB);  // the samples, written by the kernels into host memory
     StageHdr* hh = (StageHdr*)c->hstage;
+    StageHdr* hd = (StageHdr*)c->hstageDev;
     *hh = StageHdr{};
     hh->inSize = len;
     hh->count = (uint32_t)n;
     if (len) memcpy(c->hstage + hdrB, src, len);
     HIPCHK(hipMemcpyAsync(dh, c->hstage, hdrB + len, hipMemcpyHostToDevice, c->stream));
     StageHdr* d = (StageHdr*)dh;
-    rc = launch_decode(c, codec, 1, din, &d->inOff, &d->inSize, dout, &d->off0, &d->count, &d->status, c->stream,
+    rc = launch_decode(c, codec, 1, din, &d->inOff, &d->inSize, hout, &d->off0, &d->count, &hd->status, c->stream,
                        n ? (uint32_t)n : 1u);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(c->hstage, dh, sizeof(StageHdr), hipMemcpyDeviceToHost, c->stream));
-    if (n) HIPCHK(hipMemcpyAsync(c->hstage + hdrB + inB, dout, 2 * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (hh->status != PGN_OK) return hh->status;
     if (n) memcpy(dst, c->hstage + hdrB + inB, 2 * n);
