@@ -385,6 +385,8 @@ struct DecArgs {
     uint32_t segDiag;    // PGN_SEG_DIAG (timing experiments)
     uint32_t capN;       // fused kernels: as EncArgs
     const uint32_t* list;
+    uint64_t* lookback;  // small batches: the range merge's published counts / sums / results (kMergeRanges x 3 per chunk)
+    uint64_t epoch;      // this call's tag in those words (bits 48..63)
 };
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
@@ -626,6 +628,99 @@ __global__ __launch_bounds__(64 * kMergeWaves) void dec_merge_wg_kernel(DecArgs 
     if (threadIdx.x == 0) {
         if (badAny) a.status[c] = PGN_ERR_CORRUPT;
         else a.status[c] = (ph + lTot != total) ? PGN_ERR_REMAINING : PGN_OK;
+    }
+}
+
+// Small batches, many CUs per chunk: the chunk's steps in kMergeRanges ranges, one single-wave
+// workgroup each, so a lone chunk's merge runs on kMergeRanges CUs instead of one.  The ranges find
+// their places without another launch: each publishes its class counts, then (after summing those of
+// the ranges before it) the delta sum of its stream bytes, then its result, as tagged 64-bit words
+// (this call's epoch in bits 48..63) that later ranges wait for -- decoupled look-back; a workgroup
+// only waits on lower-numbered ones, which the dispatcher started first.  The last range sets the
+// status once every range is done.  Same bytes and statuses as dec_merge_wg_kernel.
+constexpr int kMergeRanges = 32;
+__device__ __forceinline__ void lb_publish(uint64_t* w, uint64_t epoch, uint64_t payload)
+{
+    __hip_atomic_store(w, (epoch << 48) | payload, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane v < nv waits for word v * 3 + k of the chunk's look-back array; returns its payload (0 for v >= nv)
+__device__ __forceinline__ uint64_t lb_wait(uint64_t* lb, int k, uint32_t nv, uint64_t epoch)
+{
+    const uint32_t v = (uint32_t)lane_id();
+    uint64_t x = 0;
+    if (v < nv) {
+        while (true) {
+            x = __hip_atomic_load(lb + 3 * v + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if ((x >> 48) == epoch) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return x & 0xFFFFFFFFFFFFull;
+}
+__global__ __launch_bounds__(64) void dec_merge_lb_kernel(DecArgs a)
+{
+    const size_t g = blockIdx.x / kMergeRanges;
+    const uint32_t r = blockIdx.x % kMergeRanges;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    if (a.status[c] != PGN_OK) return;
+    const uint32_t lane = (uint32_t)lane_id();
+    const DecUnit* d = a.units + g * kStreams;
+    uint64_t total = 0;
+    int st = PGN_OK;
+    for (int s = 0; s < kStreams; s++) {
+        if (d[s].dres < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
+        total += d[s].cs;
+    }
+    if (st != PGN_OK) {  // the same for every range of the chunk
+        if (r == 0 && lane == 0) a.status[c] = st;
+        return;
+    }
+    __shared__ MergeLds W;
+    uint64_t* lb = a.lookback + g * (3 * kMergeRanges);
+    const uint64_t ep = a.epoch;
+    const uint32_t n = a.sampleCounts[c];
+    const uint8_t* in = a.inter + g * kChunkInterBytes;
+    int16_t* out = a.samples + a.sampleOffsets[c];
+    const uint64_t dS = (uint64_t)d[1].dres, dM = (uint64_t)d[2].dres, dLl = (uint64_t)d[3].dres;
+    const uint64_t kl = ((uint64_t)n + 3) / 4;
+    const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
+    const uint32_t steps = (n + kSplitStep - 1) / kSplitStep;
+    const uint32_t s0 = (uint32_t)((uint64_t)steps * r / kMergeRanges), s1 = (uint32_t)((uint64_t)steps * (r + 1) / kMergeRanges);
+    const uint32_t t0 = s0 * kSplitStep, t1 = s1 * kSplitStep < n ? s1 * kSplitStep : n;
+    // 1. own class counts (16 bits each: a range has at most 16 steps below PGN pass sizes)
+    uint32_t cS = 0, cM = 0, cL = 0;
+    if (kl <= total) c5_class_counts(in, n, t0, t1, cS, cM, cL);
+    if (lane == 0) lb_publish(lb + 3 * r, ep, (uint64_t)cS | ((uint64_t)cM << 16) | ((uint64_t)cL << 32));
+    // 2. the counts before me -> my stream spans -> my delta sum
+    const uint64_t pc = lb_wait(lb, 0, r, ep);
+    const uint64_t sN0 = wave_sum64(pc & 0xFFFFu), mN0 = wave_sum64((pc >> 16) & 0xFFFFu), lN0 = wave_sum64(pc >> 32);
+    const uint64_t sN1 = sN0 + cS, mN1 = mN0 + cM, lN1 = lN0 + cL;
+    const bool inside = kl <= total && ps + ((sN1 + 1) >> 1) <= total && pm + mN1 <= total && pl + lN1 <= total &&
+                        ph + lN1 <= total;
+    uint32_t sum = 0;
+    if (inside) sum = c5_range_delta_sum(in, ps, pm, pl, ph, sN0, sN1, mN0, mN1, lN0, lN1);
+    if (lane == 0) lb_publish(lb + 3 * r + 1, ep, (uint64_t)sum | ((uint64_t)(inside ? 0u : 1u) << 32));
+    // 3. the running sum at my start: the sums before me; merge unless a range so far is outside
+    const uint64_t ps_ = lb_wait(lb, 1, r, ep);
+    const uint32_t carryIn = (uint32_t)wave_sum64(ps_ & 0xFFFFu);
+    const bool outsideBefore = wave_sum64((ps_ >> 32) & 1u) != 0;
+    int bad = (!inside || outsideBefore) ? 1 : 0;
+    if (!bad) {
+        uint32_t carry = carryIn;
+        uint64_t lEnd = 0;
+        bad = c5_merge_range<false>(in, total, dS, dM, dLl, out, n, t0, t1, sN0, mN0, lN0, carry, &lEnd, W);
+    }
+    if (lane == 0) lb_publish(lb + 3 * r + 2, ep, (uint64_t)(bad ? 1u : 0u));
+    // 4. the last range: every range done -> status
+    if (r == kMergeRanges - 1) {
+        const uint64_t dn = lb_wait(lb, 2, kMergeRanges, ep);
+        const bool badAny = wave_sum64(dn & 1u) != 0;
+        const uint64_t lTot = lN1;  // the class-3 count through the last range
+        if (lane == 0) {
+            __threadfence();
+            a.status[c] = badAny ? PGN_ERR_CORRUPT : ((ph + lTot != total) ? PGN_ERR_REMAINING : PGN_OK);
+        }
     }
 }
 
@@ -1241,6 +1336,8 @@ struct pgn_ctx {
     uint32_t* queues = nullptr;    // a ring of work counters, zeroed when it wraps (one per sub-batch pass)
     size_t qNext = 0;              // next unused counter of the ring
     uint32_t* qCur = nullptr;      // the current call's counters
+    uint64_t* lookback = nullptr;  // dec_merge_lb_kernel's published words (kMergeWgMaxChunks chunks)
+    uint64_t lbEpoch = 0;          // the tag of the last call that used them
     size_t nQueues = 0;
     // host-call staging: a device buffer and its pinned host mirror (same layout), so a per-chunk
     // call is one upload, the launches and one download
@@ -1411,6 +1508,7 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->encChunks);
     (void)hipFree(c->decChunks);
     (void)hipFree(c->queues);
+    (void)hipFree(c->lookback);
     (void)hipFree(c->stage);
     if (c->hstage) (void)hipHostFree(c->hstage);
     (void)hipFree(c->prof);
@@ -1740,6 +1838,21 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.segDiag = c->segDiag;
     a.capN = kPassSamples;
     a.list = nullptr;
+    a.lookback = nullptr;
+    a.epoch = 0;
+    if (G <= kMergeWgMaxChunks && codec != kCodecVbz && !c->diagNoMerge) {  // the look-back range merge
+        const size_t lbBytes = sizeof(uint64_t) * 3 * kMergeRanges * kMergeWgMaxChunks;
+        if (!c->lookback) {
+            HIPCHK(hipMalloc(&c->lookback, lbBytes));
+            HIPCHK(hipMemsetAsync(c->lookback, 0, lbBytes, s));
+        }
+        if (++c->lbEpoch > 0xFFFFu) {  // tags wrap: clear the words (ordered after every earlier call)
+            HIPCHK(hipMemsetAsync(c->lookback, 0, lbBytes, s));
+            c->lbEpoch = 1;
+        }
+        a.lookback = c->lookback;
+        a.epoch = c->lbEpoch;
+    }
     // pass p: parse + zstd on the caller's stream into buffer p % 2, merge on the side stream.  The
     // merge of pass p overlaps the zstd kernel of pass p+1; a buffer is parsed into again only after
     // the merge of the pass before last has read it.
@@ -1763,7 +1876,9 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         }
         if (c->diagNoMerge) {
         } else if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
-        else if (G <= kMergeWgMaxChunks)  // few chunks: one workgroup of kMergeWaves waves per chunk
+        else if (a.lookback)  // few chunks: kMergeRanges single-wave workgroups per chunk
+            hipLaunchKernelGGL(dec_merge_lb_kernel, dim3((unsigned)(G * kMergeRanges)), dim3(64), 0, sideS, a);
+        else if (G <= kMergeWgMaxChunks)  // one workgroup of kMergeWaves waves per chunk
             hipLaunchKernelGGL(dec_merge_wg_kernel, dim3((unsigned)G), dim3(64 * kMergeWaves), 0, sideS, a);
         else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], c->side));
