@@ -158,6 +158,8 @@ struct EncArgs {
     // large-chunk pass) or u
     uint32_t capN;
     const uint32_t* list;
+    uint64_t* lookback;  // small batches: the range split's published words (kSplitRanges x 2 per chunk)
+    uint64_t epoch;      // this call's tag in those words (bits 48..63)
 };
 
 __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
@@ -186,6 +188,96 @@ __global__ __launch_bounds__(64) void enc_split_kernel(EncArgs a)
         for (int s = 0; s < kStreams; s++) sz[s] = sizes[s];
     P.mark(0);
     P.flush();
+}
+
+// Decoupled look-back between the single-wave range workgroups of one chunk (small batches): a
+// range publishes a tagged 64-bit word (this call's epoch in bits 48..63) and later ranges wait for
+// the words of the ranges before them; a workgroup only waits on lower-numbered ones, which the
+// dispatcher started first.
+__device__ __forceinline__ void lb_publish(uint64_t* w, uint64_t epoch, uint64_t payload)
+{
+    __hip_atomic_store(w, (epoch << 48) | payload, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane v < nv waits for word v * 3 + k of the chunk's look-back array; returns its payload (0 for v >= nv)
+__device__ __forceinline__ uint64_t lb_wait(uint64_t* lb, int k, uint32_t nv, uint64_t epoch)
+{
+    const uint32_t v = (uint32_t)lane_id();
+    uint64_t x = 0;
+    if (v < nv) {
+        while (true) {
+            x = __hip_atomic_load(lb + 3 * v + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            if ((x >> 48) == epoch) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return x & 0xFFFFFFFFFFFFull;
+}
+// Small batches, many CUs per chunk: the split over kSplitRanges single-wave range workgroups.
+// Each publishes its class counts, sums those of the ranges before it (its places in the S / M /
+// class-3 streams), splits its range and publishes the nibbles the S bytes it shares need; the last
+// range writes those bytes and the stream sizes.  Same bytes as enc_split_wg_kernel.
+constexpr int kSplitRanges = 32;
+__global__ __launch_bounds__(64) void enc_split_lb_kernel(EncArgs a)
+{
+    const size_t g = blockIdx.x / kSplitRanges;
+    const uint32_t r = blockIdx.x % kSplitRanges;
+    const size_t c = a.base + g;
+    if (g >= a.G || c >= a.nchunks) return;
+    __shared__ SplitLds W;
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t n = a.sampleCounts[c];
+    uint32_t* sz = a.sizes + g * kStreams;
+    if (n > kPassSamples) {  // the large-chunk pass takes it
+        if (r == 0 && lane == 0) {
+            sz[0] = ~0u;
+            a.status[c] = PGN_ERR_UNSUPPORTED;
+            a.outSizes[c] = 0;
+        }
+        return;
+    }
+    uint64_t* lb = a.lookback + g * (3 * kSplitRanges);
+    const uint64_t ep = a.epoch;
+    const int16_t* x = a.samples + a.sampleOffsets[c];
+    uint8_t* base = a.streams + g * kChunkStreamBytes;
+    const C5Streams st{base + stream_off(0), base + stream_off(1), base + stream_off(2), base + stream_off(3),
+                       base + stream_off(4)};
+    const uint32_t steps = (n + kSplitStep - 1) / kSplitStep;
+    const uint32_t s0 = steps * r / kSplitRanges, s1 = steps * (r + 1) / kSplitRanges;
+    const uint32_t t0 = s0 * kSplitStep, t1 = s1 * kSplitStep < n ? s1 * kSplitStep : n;
+    uint32_t cS = 0, cM = 0, cL = 0;
+    if (t0 < t1) c5_split_counts(x, n, t0, t1, cS, cM, cL);
+    if (lane == 0) lb_publish(lb + 3 * r, ep, (uint64_t)cS | ((uint64_t)cM << 16) | ((uint64_t)cL << 32));
+    const uint64_t pc = lb_wait(lb, 0, r, ep);
+    const uint32_t pS = (uint32_t)wave_sum64(pc & 0xFFFFu), pM = (uint32_t)wave_sum64((pc >> 16) & 0xFFFFu),
+                   pL = (uint32_t)wave_sum64(pc >> 32);
+    uint32_t firstNib = 0xFFu, lastNib = 0xFFu;
+    if (t0 < t1) c5_split_range(x, n, t0, t1, st, pS, pM, pL, W, firstNib, lastNib);
+    if (lane == 0) lb_publish(lb + 3 * r + 1, ep, (uint64_t)(firstNib & 0xFFu) | ((uint64_t)(lastNib & 0xFFu) << 8));
+    if (r != kSplitRanges - 1) return;
+    // the last range: every range's counts and nibbles -> the shared S bytes, a trailing half byte, sizes
+    const uint64_t cnt = lb_wait(lb, 0, kSplitRanges, ep);
+    const uint64_t nb = lb_wait(lb, 1, kSplitRanges, ep);
+    const uint32_t tS = (uint32_t)wave_sum64(cnt & 0xFFFFu), tM = (uint32_t)wave_sum64((cnt >> 16) & 0xFFFFu),
+                   tL = (uint32_t)wave_sum64(cnt >> 32);
+    const uint32_t mS = (uint32_t)(cnt & 0xFFFFu);  // lane v: range v's S count
+    const uint32_t fN = (uint32_t)(nb & 0xFFu), lN = (uint32_t)((nb >> 8) & 0xFFu);
+    uint32_t at = 0, lastOwner = ~0u;
+    for (uint32_t v = 0; v < (uint32_t)kSplitRanges; v++) {  // wave-uniform walk over the ranges
+        const uint32_t cv = readlane_u32(mS, (int)v);
+        if (cv == 0) continue;
+        if ((at & 1u) && lastOwner != ~0u && lane == 0)
+            gst<uint8_t>(st.S + (at >> 1), (uint8_t)(readlane_u32(lN, (int)lastOwner) | (readlane_u32(fN, (int)v) << 4)));
+        at += cv;
+        lastOwner = v;
+    }
+    if ((at & 1u) && lastOwner != ~0u && lane == 0) gst<uint8_t>(st.S + (at >> 1), (uint8_t)readlane_u32(lN, (int)lastOwner));
+    if (lane == 0) {
+        sz[0] = (n + 3) / 4;
+        sz[1] = (tS + 1) / 2;
+        sz[2] = tM;
+        sz[3] = tL;
+        sz[4] = tL;
+    }
 }
 
 // Small batches (the per-chunk calls): one workgroup of kSplitWaves waves per chunk.  Wave w takes
@@ -639,24 +731,6 @@ __global__ __launch_bounds__(64 * kMergeWaves) void dec_merge_wg_kernel(DecArgs 
 // only waits on lower-numbered ones, which the dispatcher started first.  The last range sets the
 // status once every range is done.  Same bytes and statuses as dec_merge_wg_kernel.
 constexpr int kMergeRanges = 32;
-__device__ __forceinline__ void lb_publish(uint64_t* w, uint64_t epoch, uint64_t payload)
-{
-    __hip_atomic_store(w, (epoch << 48) | payload, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-// lane v < nv waits for word v * 3 + k of the chunk's look-back array; returns its payload (0 for v >= nv)
-__device__ __forceinline__ uint64_t lb_wait(uint64_t* lb, int k, uint32_t nv, uint64_t epoch)
-{
-    const uint32_t v = (uint32_t)lane_id();
-    uint64_t x = 0;
-    if (v < nv) {
-        while (true) {
-            x = __hip_atomic_load(lb + 3 * v + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            if ((x >> 48) == epoch) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    return x & 0xFFFFFFFFFFFFull;
-}
 __global__ __launch_bounds__(64) void dec_merge_lb_kernel(DecArgs a)
 {
     const size_t g = blockIdx.x / kMergeRanges;
@@ -1590,6 +1664,25 @@ static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
     return PGN_OK;
 }
 
+// The look-back words of the small-batch range split / merge and this call's tag.  Launch sequences
+// on a context are ordered (evLast), so one array serves every call; it is cleared when the 16-bit
+// tags wrap.
+static int take_lookback(pgn_ctx* c, hipStream_t s, uint64_t*& words, uint64_t& epoch)
+{
+    const size_t bytes = sizeof(uint64_t) * 3 * 32 * 64;  // 3 words x 32 ranges x 64 chunks
+    if (!c->lookback) {
+        HIPCHK(hipMalloc(&c->lookback, bytes));
+        HIPCHK(hipMemsetAsync(c->lookback, 0, bytes, s));
+    }
+    if (++c->lbEpoch > 0xFFFFu) {
+        HIPCHK(hipMemsetAsync(c->lookback, 0, bytes, s));
+        c->lbEpoch = 1;
+    }
+    words = c->lookback;
+    epoch = c->lbEpoch;
+    return PGN_OK;
+}
+
 // n fresh zeroed work counters for this call (c->qCur).  The counters come from a ring that is zeroed
 // only when it wraps: a per-call memset was a fill kernel plus a launch gap in front of every
 // per-chunk call.  Launch sequences on a context are ordered (evLast), so the wrap's memset runs
@@ -1763,6 +1856,12 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
     a.nu = nu;
     a.capN = kPassSamples;
     a.list = nullptr;
+    a.lookback = nullptr;
+    a.epoch = 0;
+    if (G <= kSplitWgMaxChunks && codec != kCodecVbz) {  // the look-back range split
+        rc = take_lookback(c, s, a.lookback, a.epoch);
+        if (rc) return rc;
+    }
     // pass p: split on the side stream into buffer p % 2; zstd + assemble on the caller's stream.
     // The split of pass p+1 overlaps the zstd kernel of pass p; a buffer is split into again only
     // after the assemble kernel of the pass before last has read it.
@@ -1777,7 +1876,9 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
         a.queue = c->qCur + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(c->side, c->evFree[b], 0));
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
-        else if (G <= kSplitWgMaxChunks)  // few chunks: one workgroup of kSplitWaves waves per chunk
+        else if (a.lookback)  // few chunks: kSplitRanges single-wave workgroups per chunk
+            hipLaunchKernelGGL(enc_split_lb_kernel, dim3((unsigned)(G * kSplitRanges)), dim3(64), 0, sideS, a);
+        else if (G <= kSplitWgMaxChunks)  // one workgroup of kSplitWaves waves per chunk
             hipLaunchKernelGGL(enc_split_wg_kernel, dim3((unsigned)G), dim3(64 * kSplitWaves), 0, sideS, a);
         else hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         if (passes > 1) {
@@ -1841,17 +1942,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.lookback = nullptr;
     a.epoch = 0;
     if (G <= kMergeWgMaxChunks && codec != kCodecVbz && !c->diagNoMerge) {  // the look-back range merge
-        const size_t lbBytes = sizeof(uint64_t) * 3 * kMergeRanges * kMergeWgMaxChunks;
-        if (!c->lookback) {
-            HIPCHK(hipMalloc(&c->lookback, lbBytes));
-            HIPCHK(hipMemsetAsync(c->lookback, 0, lbBytes, s));
-        }
-        if (++c->lbEpoch > 0xFFFFu) {  // tags wrap: clear the words (ordered after every earlier call)
-            HIPCHK(hipMemsetAsync(c->lookback, 0, lbBytes, s));
-            c->lbEpoch = 1;
-        }
-        a.lookback = c->lookback;
-        a.epoch = c->lbEpoch;
+        const int lrc = take_lookback(c, s, a.lookback, a.epoch);
+        if (lrc) return lrc;
     }
     // pass p: parse + zstd on the caller's stream into buffer p % 2, merge on the side stream.  The
     // merge of pass p overlaps the zstd kernel of pass p+1; a buffer is parsed into again only after
