@@ -52,7 +52,6 @@ struct HufRd {
 // one wave per stream) gives each wave its own rows in its kernel's LDS, passed as an LDS pointer (an
 // LDS variable named by non-kernel functions of several kernels would move the others' LDS behind
 // a per-kernel offset table).
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
 __device__ __forceinline__ uint32_t stg_word(const lds_u32* stg, int32_t row, int lane)
 {
     return stg[64 * row + lane];

@@ -374,6 +374,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
     S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
     S.maxSeq = kMaxEncSeq;
     S.huf = (uint32_t*)(sbase + lay.huf);
+    S.coop = nullptr;
     uint32_t epoch = a.epochs[blockIdx.x];  // table state: epoch tag | written extent << 8 (ht_next_epoch)
     PhaseProf P;
     P.init(a.prof);
@@ -397,6 +398,56 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
         wave_sync();
     }
     if (lane == 0) a.epochs[blockIdx.x] = epoch;
+    P.flush();
+}
+
+// Small batches (the per-chunk calls): one workgroup of kCoopEncWaves waves per stream.  Wave 0
+// compresses the stream; the histograms and the bit packing of its four-segment literals sections
+// are shared with the other waves, one segment each (pgn_zenc.h CoopEncCmd).  A lone chunk's encode
+// is bound by its largest stream's frame.
+__global__ __launch_bounds__(64 * kCoopEncWaves) void enc_zstd_coop_kernel(EncArgs a)
+{
+    const int lane = lane_id();
+    const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const size_t G = a.G;
+    const uint32_t u = blockIdx.x;
+    if ((size_t)u >= (size_t)a.nu * G) return;
+    const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
+    const size_t g = u % G;
+    if (a.base + g >= a.nchunks) return;
+    if (a.sizes[g * kStreams] == ~0u) return;  // unsupported chunk (the same for every wave)
+    __shared__ uint32_t winAll[(kCoopEncWaves - 1) * kWinWords];
+    __shared__ CoopEncCmd cmdLds;
+    lds_enc_cmd* cmd = (lds_enc_cmd*)&cmdLds;
+    if (wid != 0) {
+        coop_enc_helper_wave(wid, cmd, (lds_u32*)&winAll[(wid - 1) * kWinWords]);
+        return;
+    }
+    const EncLayout lay = enc_layout();
+    uint8_t* sbase = a.slotScratch + (size_t)u * a.slotBytes;
+    EncScratch S;
+    S.ht = (uint32_t*)(sbase + lay.ht);
+    S.seqs = (z1::Seq*)(sbase + lay.seqs);
+    S.codes = sbase + lay.codes;
+    S.lit = sbase + lay.lit;
+    S.seqSection = sbase + lay.seqSection;
+    S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
+    S.maxSeq = kMaxEncSeq;
+    S.huf = (uint32_t*)(sbase + lay.huf);
+    S.coop = cmd;
+    uint32_t epoch = a.epochs[u];  // table state of slot u (ht_next_epoch)
+    PhaseProf P;
+    P.init(a.prof);
+    const uint32_t n = a.sizes[g * kStreams + s];
+    ht_next_epoch(S.ht, epoch, n);
+    const uint8_t* src = a.streams + g * kChunkStreamBytes + (a.nu == 1 ? a.sizes[g * kStreams + 1] : stream_off(s));
+    uint8_t* dst = a.frames + g * kChunkFrameBytes + frame_off(s);
+    const size_t fsz = zstd1_compress_wave<true>(dst, src, n, S, epoch & 0xFFu, P);
+    if (lane == 0) {
+        a.fsizes[g * kStreams + s] = (uint32_t)fsz;
+        a.epochs[u] = epoch;
+    }
+    coop_enc_finish(cmd);
     P.flush();
 }
 
@@ -1050,6 +1101,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void en
     S.seqWork = (z1::SeqWork*)(sbase + lay.seqWork);
     S.maxSeq = kMaxEncSeq;
     S.huf = (uint32_t*)(sbase + lay.huf);
+    S.coop = nullptr;
     const uint32_t capN = a.capN;
     uint8_t* streams = sbase + lay.bytes;
     uint8_t* fbuf = streams + chunk_stream_bytes(capN);
@@ -1885,7 +1937,9 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
             HIPCHK(hipEventRecord(c->evStage[b], c->side));
             HIPCHK(hipStreamWaitEvent(s, c->evStage[b], 0));
         }
-        hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+        if (G <= kSplitWgMaxChunks && (size_t)nu * G <= slots)  // few chunks: a workgroup per stream
+            hipLaunchKernelGGL(enc_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopEncWaves), 0, s, a);
+        else hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
         else hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
         if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], s));

@@ -13,6 +13,8 @@ namespace pgn {
 // each, so adding a decode kernel moved the encoder's behind the table: encode +4 %).  One variable
 // reached by every codec kernel sits at offset 0 in each of them.
 constexpr size_t kCodecLdsBytes = 8192;
+// an LDS word pointer (cooperative kernels pass their own LDS to the shared device functions this way)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 static __shared__ __attribute__((aligned(16))) uint8_t sCodecLds[kCodecLdsBytes];
 
 constexpr int kWave = 64;

@@ -101,6 +101,7 @@ struct EncScratch {
     z1::SeqWork* seqWork;
     uint32_t maxSeq;
     uint32_t* huf;       // two Huffman tables (code | nbBits << 16, 256 each): confirmed and candidate
+    struct CoopEncCmd __attribute__((address_space(3)))* coop;  // cooperative encode: the post (else null)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -523,7 +524,7 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
 // as coalesced dword stores.
 // ---------------------------------------------------------------------------------------------
 __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, const uint8_t* __restrict__ src, uint32_t len,
-                                                     uint32_t totalBits)
+                                                     uint32_t totalBits, lds_u32* win)
 {
     const uint32_t lane = (uint32_t)lane_id();
     out = uni(out);
@@ -531,7 +532,6 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
     len = uni(len);
     totalBits = uni(totalBits);
     const uint32_t* cw = sEnc.cw;
-    uint32_t* win = sEnc.win;
     for (uint32_t w = lane; w < (uint32_t)kWinWords; w += 64) win[w] = 0;
     lds_sync();
     uint32_t winLo = 0;   // bit offset of win[0] (multiple of 32)
@@ -588,9 +588,10 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
         for (int g = 0; g < 4; g++) {
             const uint32_t w = pos >> 5, sh = pos & 31;
             const uint64_t lo = grp[g] << sh;
-            atomicOr(&win[w], (uint32_t)lo);
-            atomicOr(&win[w + 1], (uint32_t)(lo >> 32));
-            atomicOr(&win[w + 2], (uint32_t)((grp[g] >> 32) >> (32 - sh)));
+            __hip_atomic_fetch_or(&win[w], (uint32_t)lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_or(&win[w + 1], (uint32_t)(lo >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_fetch_or(&win[w + 2], (uint32_t)((grp[g] >> 32) >> (32 - sh)), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
             pos += gnb[g];
         }
         lds_sync();
@@ -619,6 +620,84 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
     uint8_t* o = out + (winLo >> 3);
     for (uint32_t b = lane; b < nbytes; b += 64) gst<uint8_t>(o + b, (uint8_t)(win[b >> 2] >> (8 * (b & 3))));
     lds_sync();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Cooperative encode (small batches, enc_zstd_coop_kernel): a workgroup of kCoopEncWaves waves per
+// stream.  Wave 0 runs zstd1_compress_wave<true>; a four-segment literals section's histograms and
+// its bit packing are posted here, and wave k does segment k (its own bit window); the rest is wave 0's.
+// ---------------------------------------------------------------------------------------------
+constexpr int kCoopEncWaves = 4;
+struct CoopEncCmd {
+    uint32_t op;  // 0: done, 1: segment histograms, 2: segment bit packing
+    uint32_t n, segSize;
+    const uint8_t* lit;
+    uint8_t* out[4];
+    uint32_t bits[4];
+};
+typedef __attribute__((address_space(3))) CoopEncCmd lds_enc_cmd;
+
+// the histogram of literals segment k ([k segSize, min((k + 1) segSize, n))) into sEnc.hist2, whose
+// other segments other waves add at the same time (LDS atomics)
+__device__ __noinline__ void hist_segment_wave(const uint8_t* __restrict__ lit, uint32_t n, uint32_t segSize, uint32_t k)
+{
+    EncLds& L = sEnc;
+    const uint32_t lane = (uint32_t)lane_id();
+    lit = uni(lit);
+    n = uni(n);
+    segSize = uni(segSize);
+    k = uni(k);
+    const uint32_t a0 = k * segSize, a1 = (k + 1) * segSize < n ? (k + 1) * segSize : n;
+    uint32_t* h = &L.hist2[k >> 1][0];
+    const uint32_t inc = 1u << (16 * (k & 1));
+    for (uint32_t i0 = a0 + 16u * lane; i0 < a1; i0 += 4096) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 1024u * (uint32_t)u;
+            if (i + 16 <= a1) {
+                v[u] = gld<uint4>(lit + i);
+            } else {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (uint32_t b = 0; b < 16; b++)
+                    if (i + b < a1) w[b >> 2] |= (uint32_t)gb(lit + i + b) << (8 * (b & 3));
+                v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 1024u * (uint32_t)u;
+            const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            if (i + 16 <= a1) {
+#pragma unroll
+                for (int b = 0; b < 16; b++) atomicAdd(h + ((wd[b >> 2] >> (8 * (b & 3))) & 0xFFu), inc);
+            } else {
+                for (uint32_t b = 0; b < 16; b++)
+                    if (i + b < a1) atomicAdd(h + ((wd[b >> 2] >> (8 * (b & 3))) & 0xFFu), inc);
+            }
+        }
+    }
+}
+
+// waves 1..3 of a cooperative encode workgroup
+__device__ __noinline__ void coop_enc_helper_wave(uint32_t wid, lds_enc_cmd* cmd, lds_u32* win)
+{
+    while (true) {
+        __syncthreads();  // B1: a job (or done) is posted
+        const uint32_t op = cmd->op;
+        if (op == 0) break;
+        if (op == 1) hist_segment_wave(cmd->lit, cmd->n, cmd->segSize, wid);
+        else {
+            const uint32_t a = cmd->segSize * wid, e = wid == 3 ? cmd->n : a + cmd->segSize;
+            huf_encode_segment_wave(cmd->out[wid], cmd->lit + a, e - a, cmd->bits[wid], win);
+        }
+        __syncthreads();  // B2
+    }
+}
+__device__ __forceinline__ void coop_enc_finish(lds_enc_cmd* cmd)
+{
+    if (lane_id() == 0) cmd->op = 0;
+    __syncthreads();  // B1 with op 0
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1388,10 +1467,11 @@ struct LitOut {
     uint32_t size;
     uint32_t newTable;  // a new table was built and used (HUF_repeat_check from here on)
 };
+template <bool COOP>
 __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ lit, uint32_t n,
                                                       PhaseProf& P, uint32_t writeRaw, const uint32_t* prevCw,
                                                       uint32_t prevCheck, uint32_t* nextCw, uint32_t saveNew,
-                                                      uint32_t rawAt)
+                                                      uint32_t rawAt, lds_enc_cmd* coop)
 {
     EncLds& L = sEnc;
     dst = uni(dst);
@@ -1417,8 +1497,19 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     const int nseg = single ? 1 : 4;
     for (int i = lane; i < 2 * 256; i += 64) (&L.hist2[0][0])[i] = 0;
     wave_sync();
+    if (COOP && !single) {  // the four segments' histograms on the four waves
+        if (lane == 0) {
+            coop->op = 1;
+            coop->lit = lit;
+            coop->n = n;
+            coop->segSize = segSize;
+        }
+        __syncthreads();  // B1
+        hist_segment_wave(lit, n, segSize, 0);
+        __syncthreads();  // B2
+    }
     // per-segment histograms; the 16-byte loads of four 1024-byte steps are issued together
-    for (uint32_t i0 = (uint32_t)lane * 16; i0 < n; i0 += 4096) {
+    for (uint32_t i0 = (uint32_t)lane * 16; i0 < ((COOP && !single) ? 0u : n); i0 += 4096) {
         uint4 v[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -1636,14 +1727,32 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     for (uint32_t i = (uint32_t)lane; i < hSize; i += 64) gst<uint8_t>(dst + lhSize + i, L.hdr[i]);
     wave_sync();
     uint8_t* op = dst + lhSize + hSize + (single ? 0 : 6);
-    for (int k = 0; k < nseg; k++) {
-        uint32_t a = segSize * (uint32_t)k;
-        uint32_t e = (k == nseg - 1) ? n : a + segSize;
+    if (COOP && !single) {  // the four segments' bit packing on the four waves
+        if (lane == 0) {
+            coop->op = 2;
+            coop->lit = lit;
+            coop->n = n;
+            coop->segSize = segSize;
+            uint8_t* o = op;
+            for (int k = 0; k < 4; k++) {
+                coop->out[k] = o;
+                coop->bits[k] = bits[k];
+                o += bytes[k];
+            }
+        }
+        __syncthreads();  // B1
+        huf_encode_segment_wave(op, lit, segSize, bits[0], (lds_u32*)sEnc.win);
+        __syncthreads();  // B2
+    } else {
+        for (int k = 0; k < nseg; k++) {
+            uint32_t a = segSize * (uint32_t)k;
+            uint32_t e = (k == nseg - 1) ? n : a + segSize;
 #if PGN_AB_SKIP != 4
-        huf_encode_segment_wave(op, lit + a, e - a, bits[k]);
+            huf_encode_segment_wave(op, lit + a, e - a, bits[k], (lds_u32*)sEnc.win);
 #endif
-        P.count(7, (e - a + 1023) / 1024);
-        op += bytes[k];
+            P.count(7, (e - a + 1023) / 1024);
+            op += bytes[k];
+        }
     }
     P.mark(6);
     return ret(lhSize + total, !useOld);
@@ -1663,6 +1772,7 @@ __device__ inline bool wave_is_rle(const uint8_t* p, uint32_t n)  // ZSTD_isRLE
     return !ballot(diff);
 }
 
+template <bool COOP = false>
 __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t n,
                                              EncScratch S, uint32_t tag, PhaseProf& P)
 {
@@ -1741,9 +1851,9 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
             // is then only sized here, and the raw block below is the one copy
             // without sequences the block is compressed only if litSize + 1 < maxCSize
             const uint32_t maxCSize = bs - ((bs >> 6) + 2);
-            const LitOut lo = compress_literals_wave(body, lit, nLit, P, nbSeq > 0 ? 1u : 0u, S.huf + 256 * hufCur, hufCheck,
-                                                     S.huf + 256 * (hufCur ^ 1u), last ? 0u : 1u,
-                                                     nbSeq == 0 ? maxCSize - 1u : 0xFFFFFFFFu);
+            const LitOut lo = compress_literals_wave<COOP>(body, lit, nLit, P, nbSeq > 0 ? 1u : 0u, S.huf + 256 * hufCur,
+                                                           hufCheck, S.huf + 256 * (hufCur ^ 1u), last ? 0u : 1u,
+                                                           nbSeq == 0 ? maxCSize - 1u : 0xFFFFFFFFu, S.coop);
             const size_t litSize = uni(lo.size);
             wave_sync();
             if (nbSeq == 0) {
