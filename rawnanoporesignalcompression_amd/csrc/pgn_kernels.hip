@@ -530,6 +530,7 @@ struct DecArgs {
     const uint32_t* list;
     uint64_t* lookback;  // small batches: the range merge's published counts / sums / results (kMergeRanges x 3 per chunk)
     uint64_t epoch;      // this call's tag in those words (bits 48..63)
+    uint32_t coopParse;  // dec_zstd_coop_kernel parses the chunks itself (no dec_parse_kernel launch)
 };
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
@@ -629,7 +630,36 @@ __global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs 
     const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
     const size_t g = u % G;
     const size_t c = a.base + g;
-    if (c >= a.nchunks || a.status[c] != PGN_OK) return;  // the same for every wave of the group
+    if (c >= a.nchunks) return;
+    __shared__ int32_t parseRc;
+    __shared__ DecUnit myUnit;
+    if (a.coopParse) {  // the chunk's prefixes and frame headers (dec_parse_kernel's work), here
+        if (threadIdx.x == 0) {
+            DecUnit uu[kStreams];
+            const int rc = a.sampleCounts[c] > kPassSamples ? PGN_ERR_UNSUPPORTED
+                                                            : c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], uu);
+            parseRc = rc;
+            if (rc == PGN_OK) myUnit = uu[s];
+            if (s == 0) {  // the chunk's first frame publishes its status and frame records for the merge
+                a.status[c] = rc;
+                if (rc == PGN_OK) {
+                    for (int k = 0; k < kStreams; k++) {
+                        DecUnit& w = a.units[g * kStreams + k];
+                        w.src = uu[k].src;
+                        w.len = uu[k].len;
+                        w.cs = uu[k].cs;
+                        w.interOff = uu[k].interOff;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (parseRc != PGN_OK) return;  // the same for every wave of the group
+    } else {
+        if (a.status[c] != PGN_OK) return;
+        if (threadIdx.x == 0) myUnit = a.units[g * kStreams + s];
+        __syncthreads();
+    }
     PhaseProf P;
     P.init(a.prof);
     __shared__ uint32_t stgAll[kCoopWaves * kCoopStgWords];
@@ -656,10 +686,11 @@ __global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs 
     S.segDiag = 0;
     S.coopCmd = cmd;
     S.coopStg = stg;
-    DecUnit& d = a.units[g * kStreams + s];
-    const size_t cap = a.nu == 1 ? (size_t)d.cs + kVbzPadding : (size_t)d.cs;
-    const long r = zstd_decompress_wave<true>(a.in + d.src, d.len, a.inter + g * kChunkInterBytes + d.interOff, cap, S, P);
-    if (lane == 0) d.dres = (int32_t)r;
+    const uint64_t dsrc = myUnit.src;
+    const uint32_t dlen = myUnit.len, dcs = myUnit.cs, doff = myUnit.interOff;
+    const size_t cap = a.nu == 1 ? (size_t)dcs + kVbzPadding : (size_t)dcs;
+    const long r = zstd_decompress_wave<true>(a.in + dsrc, dlen, a.inter + g * kChunkInterBytes + doff, cap, S, P);
+    if (lane == 0) a.units[g * kStreams + s].dres = (int32_t)r;
     coop_finish(cmd);
     P.flush();
 }
@@ -2011,9 +2042,11 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         a.base = p * G;
         a.queue = c->qCur + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(s, c->evFree[b], 0));
+        const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots && !c->hufSegCap;
+        a.coopParse = (coop && codec != kCodecVbz) ? 1u : 0u;
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
-        if (G <= kCoopMaxChunks && (size_t)nu * G <= slots && !c->hufSegCap)  // few chunks: a workgroup per frame
+        else if (!a.coopParse) hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
+        if (coop)  // few chunks: a workgroup per frame
             hipLaunchKernelGGL(dec_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopWaves), 0, s, a);
         else hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
         if (passes > 1) {
