@@ -567,7 +567,7 @@ struct MergePlan {
 // The merge of the steps [t0, t1) of a chunk (t0 a multiple of kSplitStep, t1 = n or one), given
 // the class counts of the samples before t0 (sN0 / mN0 / lN0) and the running sum there (carry, in
 // and out); *lEnd receives the class-3 count through t1.  c5_merge_wave is the whole chunk in one
-// call; dec_merge_wg_kernel gives the ranges of one chunk to the waves of a workgroup.
+// call; dec_merge_lb_kernel gives the ranges of one chunk to single-wave workgroups.
 template <bool C4 = false>
 __device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
                                               uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint32_t t0,

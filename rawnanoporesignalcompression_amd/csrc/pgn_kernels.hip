@@ -215,7 +215,7 @@ __device__ __forceinline__ uint64_t lb_wait(uint64_t* lb, int k, uint32_t nv, ui
 // Small batches, many CUs per chunk: the split over kSplitRanges single-wave range workgroups.
 // Each publishes its class counts, sums those of the ranges before it (its places in the S / M /
 // class-3 streams), splits its range and publishes the nibbles the S bytes it shares need; the last
-// range writes those bytes and the stream sizes.  Same bytes as enc_split_wg_kernel.
+// range writes those bytes and the stream sizes.  Same bytes as enc_split_kernel.
 constexpr int kSplitRanges = 32;
 __global__ __launch_bounds__(64) void enc_split_lb_kernel(EncArgs a)
 {
@@ -280,85 +280,7 @@ __global__ __launch_bounds__(64) void enc_split_lb_kernel(EncArgs a)
     }
 }
 
-// Small batches (the per-chunk calls): one workgroup of kSplitWaves waves per chunk.  Wave w takes
-// about 1/kSplitWaves of the chunk's 1,024-sample steps; the class counts of every range (from the
-// samples) place each range in the S / M / class-3 streams; the waves split their ranges at once;
-// then the S bytes shared by two ranges (an odd nibble start) and a trailing half byte are written
-// from the nibbles the waves handed over.
-constexpr int kSplitWaves = 8;
-constexpr size_t kSplitWgMaxChunks = 64;  // batches up to this many chunks use it
-__global__ __launch_bounds__(64 * kSplitWaves) void enc_split_wg_kernel(EncArgs a)
-{
-    const size_t g = blockIdx.x;
-    const size_t c = a.base + g;
-    if (g >= a.G || c >= a.nchunks) return;
-    __shared__ SplitLds Wv[kSplitWaves];
-    __shared__ uint32_t cnt[kSplitWaves][3];
-    __shared__ uint32_t nibs[kSplitWaves][2];
-    const uint32_t w = threadIdx.x >> 6;
-    const uint32_t lane = (uint32_t)lane_id();
-    const uint32_t n = a.sampleCounts[c];
-    uint32_t* sz = a.sizes + g * kStreams;
-    if (n > kPassSamples) {  // the large-chunk pass takes it
-        if (threadIdx.x == 0) {
-            sz[0] = ~0u;
-            a.status[c] = PGN_ERR_UNSUPPORTED;
-            a.outSizes[c] = 0;
-        }
-        return;
-    }
-    const int16_t* x = a.samples + a.sampleOffsets[c];
-    uint8_t* base = a.streams + g * kChunkStreamBytes;
-    const C5Streams st{base + stream_off(0), base + stream_off(1), base + stream_off(2), base + stream_off(3),
-                       base + stream_off(4)};
-    const uint32_t steps = (n + kSplitStep - 1) / kSplitStep;
-    const uint32_t s0 = steps * w / kSplitWaves, s1 = steps * (w + 1) / kSplitWaves;
-    const uint32_t t0 = s0 * kSplitStep, t1 = s1 * kSplitStep < n ? s1 * kSplitStep : n;
-    uint32_t cS = 0, cM = 0, cL = 0;
-    c5_split_counts(x, n, t0, t1, cS, cM, cL);
-    if (lane == 0) {
-        cnt[w][0] = cS;
-        cnt[w][1] = cM;
-        cnt[w][2] = cL;
-    }
-    __syncthreads();
-    uint32_t pS = 0, pM = 0, pL = 0, tS = 0, tM = 0, tL = 0;
-    for (uint32_t v = 0; v < (uint32_t)kSplitWaves; v++) {
-        if (v < w) {
-            pS += cnt[v][0];
-            pM += cnt[v][1];
-            pL += cnt[v][2];
-        }
-        tS += cnt[v][0];
-        tM += cnt[v][1];
-        tL += cnt[v][2];
-    }
-    uint32_t firstNib = 0xFFu, lastNib = 0xFFu;
-    if (t0 < t1) c5_split_range(x, n, t0, t1, st, pS, pM, pL, Wv[w], firstNib, lastNib);
-    if (lane == 0) {
-        nibs[w][0] = firstNib;
-        nibs[w][1] = lastNib;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        // the S bytes two ranges share, then a trailing half byte (its high nibble zero)
-        uint32_t at = 0, lastOwner = ~0u;
-        for (uint32_t v = 0; v < (uint32_t)kSplitWaves; v++) {
-            if (cnt[v][0] == 0) continue;
-            if ((at & 1u) && lastOwner != ~0u)
-                gst<uint8_t>(st.S + (at >> 1), (uint8_t)(nibs[lastOwner][1] | (nibs[v][0] << 4)));
-            at += cnt[v][0];
-            lastOwner = v;
-        }
-        // the stream's odd end (a byte of its own: with an odd start the last range's count is even)
-        if ((at & 1u) && lastOwner != ~0u) gst<uint8_t>(st.S + (at >> 1), (uint8_t)nibs[lastOwner][1]);
-        sz[0] = (n + 3) / 4;
-        sz[1] = (tS + 1) / 2;
-        sz[2] = tM;
-        sz[3] = tL;
-        sz[4] = tL;
-    }
-}
+constexpr size_t kSplitWgMaxChunks = 64;  // batches up to this many chunks take the small-batch kernels
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void enc_zstd_kernel(EncArgs a)
 {
@@ -723,87 +645,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void de
     P.flush();
 }
 
-// Small batches (the per-chunk calls): one workgroup of kMergeWaves waves per chunk.  Wave w takes
-// about 1/kMergeWaves of the chunk's 1,024-sample steps.  The class counts of every range (from its
-// keys) place each range in the S / M / class-3 streams; the delta sums of the ranges before a
-// wave's own (an order-free reduction over their stream bytes) give its running sum at entry; then
-// the waves merge their ranges at once.  Same statuses as dec_merge_kernel.
-constexpr int kMergeWaves = 16;
-constexpr size_t kMergeWgMaxChunks = 64;  // batches up to this many chunks use it
-__global__ __launch_bounds__(64 * kMergeWaves) void dec_merge_wg_kernel(DecArgs a)
-{
-    const size_t g = blockIdx.x;
-    const size_t c = a.base + g;
-    if (g >= a.G || c >= a.nchunks) return;
-    if (a.status[c] != PGN_OK) return;
-    __shared__ MergeLds Wv[kMergeWaves];
-    __shared__ uint32_t cnt[kMergeWaves][3];
-    __shared__ uint32_t sums[kMergeWaves];
-    __shared__ uint32_t badAny;
-    const uint32_t w = threadIdx.x >> 6;
-    const uint32_t lane = (uint32_t)lane_id();
-    const DecUnit* d = a.units + g * kStreams;
-    uint64_t total = 0;
-    int st = PGN_OK;
-    for (int s = 0; s < kStreams; s++) {
-        if (d[s].dres < 0) st = PGN_ERR_ZSTD_DECOMPRESS;
-        total += d[s].cs;
-    }
-    if (st != PGN_OK) {  // the same for every wave of the workgroup
-        if (threadIdx.x == 0) a.status[c] = st;
-        return;
-    }
-    const uint32_t n = a.sampleCounts[c];
-    const uint8_t* in = a.inter + g * kChunkInterBytes;
-    int16_t* out = a.samples + a.sampleOffsets[c];
-    const uint64_t dS = (uint64_t)d[1].dres, dM = (uint64_t)d[2].dres, dLl = (uint64_t)d[3].dres;
-    const uint64_t kl = ((uint64_t)n + 3) / 4;
-    const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
-    const uint32_t steps = (n + kSplitStep - 1) / kSplitStep;
-    const uint32_t s0 = (uint32_t)((uint64_t)steps * w / kMergeWaves), s1 = (uint32_t)((uint64_t)steps * (w + 1) / kMergeWaves);
-    const uint32_t t0 = s0 * kSplitStep, t1 = s1 * kSplitStep < n ? s1 * kSplitStep : n;
-    if (threadIdx.x == 0) badAny = kl > total ? 1u : 0u;  // the keys alone run past the streams
-    uint32_t cS = 0, cM = 0, cL = 0;
-    if (kl <= total) c5_class_counts(in, n, t0, t1, cS, cM, cL);
-    if (lane == 0) {
-        cnt[w][0] = cS;
-        cnt[w][1] = cM;
-        cnt[w][2] = cL;
-    }
-    __syncthreads();
-    uint64_t sN0 = 0, mN0 = 0, lN0 = 0, lTot = 0;
-    for (uint32_t v = 0; v < (uint32_t)kMergeWaves; v++) {
-        if (v < w) {
-            sN0 += cnt[v][0];
-            mN0 += cnt[v][1];
-            lN0 += cnt[v][2];
-        }
-        lTot += cnt[v][2];
-    }
-    const uint64_t sN1 = sN0 + cS, mN1 = mN0 + cM, lN1 = lN0 + cL;
-    // my range's stream bytes must lie inside the intermediate (else the one-wave merge fails too)
-    const bool inside = ps + ((sN1 + 1) >> 1) <= total && pm + mN1 <= total && pl + lN1 <= total && ph + lN1 <= total;
-    uint32_t sum = 0;
-    if (inside && kl <= total) sum = c5_range_delta_sum(in, ps, pm, pl, ph, sN0, sN1, mN0, mN1, lN0, lN1);
-    if (lane == 0) {
-        sums[w] = sum;
-        if (!inside) atomicOr(&badAny, 1u);
-    }
-    __syncthreads();
-    int bad = badAny != 0;
-    if (!bad) {
-        uint32_t carry = 0;
-        for (uint32_t v = 0; v < w; v++) carry += sums[v];
-        uint64_t lEnd = 0;
-        bad = c5_merge_range<false>(in, total, dS, dM, dLl, out, n, t0, t1, sN0, mN0, lN0, carry, &lEnd, Wv[w]);
-        if (bad && lane == 0) atomicOr(&badAny, 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (badAny) a.status[c] = PGN_ERR_CORRUPT;
-        else a.status[c] = (ph + lTot != total) ? PGN_ERR_REMAINING : PGN_OK;
-    }
-}
+constexpr size_t kMergeWgMaxChunks = 64;  // batches up to this many chunks take the small-batch kernels
 
 // Small batches, many CUs per chunk: the chunk's steps in kMergeRanges ranges, one single-wave
 // workgroup each, so a lone chunk's merge runs on kMergeRanges CUs instead of one.  The ranges find
@@ -811,7 +653,7 @@ __global__ __launch_bounds__(64 * kMergeWaves) void dec_merge_wg_kernel(DecArgs 
 // the ranges before it) the delta sum of its stream bytes, then its result, as tagged 64-bit words
 // (this call's epoch in bits 48..63) that later ranges wait for -- decoupled look-back; a workgroup
 // only waits on lower-numbered ones, which the dispatcher started first.  The last range sets the
-// status once every range is done.  Same bytes and statuses as dec_merge_wg_kernel.
+// status once every range is done.  Same bytes and statuses as dec_merge_kernel.
 constexpr int kMergeRanges = 32;
 __global__ __launch_bounds__(64) void dec_merge_lb_kernel(DecArgs a)
 {
@@ -1961,8 +1803,6 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         else if (a.lookback)  // few chunks: kSplitRanges single-wave workgroups per chunk
             hipLaunchKernelGGL(enc_split_lb_kernel, dim3((unsigned)(G * kSplitRanges)), dim3(64), 0, sideS, a);
-        else if (G <= kSplitWgMaxChunks)  // one workgroup of kSplitWaves waves per chunk
-            hipLaunchKernelGGL(enc_split_wg_kernel, dim3((unsigned)G), dim3(64 * kSplitWaves), 0, sideS, a);
         else hipLaunchKernelGGL(enc_split_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         if (passes > 1) {
             HIPCHK(hipEventRecord(c->evStage[b], c->side));
@@ -2057,8 +1897,6 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         } else if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         else if (a.lookback)  // few chunks: kMergeRanges single-wave workgroups per chunk
             hipLaunchKernelGGL(dec_merge_lb_kernel, dim3((unsigned)(G * kMergeRanges)), dim3(64), 0, sideS, a);
-        else if (G <= kMergeWgMaxChunks)  // one workgroup of kMergeWaves waves per chunk
-            hipLaunchKernelGGL(dec_merge_wg_kernel, dim3((unsigned)G), dim3(64 * kMergeWaves), 0, sideS, a);
         else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], c->side));
     }
