@@ -323,6 +323,44 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
     P.flush();
 }
 
+// The small-batch C5 encode places its frames itself (no enc_assemble_kernel): frame s publishes
+// its size in look-back word 3 s + 2 of its chunk, waits for the sizes of frames 0 .. s-1 (lower
+// workgroups, dispatched first), and copies itself behind their length prefixes (C5.hpp:429-462)
+// when it fits the capacity.  Frame 4 then knows the total and writes the status, the size and the
+// stats as enc_assemble_kernel does.  On DST_TOO_SMALL the bytes that fit may have been written
+// (as in the fused kernel, which writes its frames straight into the blob).
+__device__ __noinline__ void enc_place_frame(const EncArgs& a, size_t g, int s, const uint8_t* fr, uint32_t f)
+{
+    const size_t c = a.base + g;
+    const int lane = lane_id();
+    uint64_t* lb = a.lookback + g * (3 * kSplitRanges);
+    const uint64_t ep = a.epoch;
+    if (lane == 0) lb_publish(lb + 3 * s + 2, ep, f);
+    const uint64_t fv = lb_wait(lb, 2, (uint32_t)s, ep);  // lane v < s: frame v's size
+    const uint64_t off = wave_sum64(fv) + 8ull * (uint64_t)s;
+    const uint32_t pre = s < kStreams - 1 ? 8u : 0u;
+    const uint64_t cap = a.outCaps[c];
+    uint8_t* out = a.out + a.outOffsets[c];
+    if (off + pre + f <= cap) {
+        if (pre && lane == 0) {
+            const uint64_t v = f;
+            __builtin_memcpy(out + off, &v, 8);
+        }
+        wave_copy(out + off + pre, fr, f);
+    }
+    if (s != kStreams - 1) return;
+    const uint64_t total = off + f;
+    const uint32_t* sz = a.sizes + g * kStreams;
+    if (lane == 0) {
+        a.status[c] = total <= cap ? PGN_OK : PGN_ERR_DST_TOO_SMALL;
+        a.outSizes[c] = total;
+    }
+    if (a.stats && lane < kStreams) {
+        a.stats[c * PGN_STATS_PER_CHUNK + lane] = sz[lane];
+        a.stats[c * PGN_STATS_PER_CHUNK + 5 + lane] = lane == kStreams - 1 ? f : (uint32_t)fv;
+    }
+}
+
 // Small batches (the per-chunk calls): one workgroup of kCoopEncWaves waves per stream.  Wave 0
 // compresses the stream; the histograms and the bit packing of its four-segment literals sections
 // are shared with the other waves, one segment each (pgn_zenc.h CoopEncCmd).  A lone chunk's encode
@@ -370,6 +408,7 @@ __global__ __launch_bounds__(64 * kCoopEncWaves) void enc_zstd_coop_kernel(EncAr
         a.epochs[u] = epoch;
     }
     coop_enc_finish(cmd);
+    if (a.lookback) enc_place_frame(a, g, s, dst, (uint32_t)fsz);  // C5 (the look-back split ran)
     P.flush();
 }
 
@@ -1783,7 +1822,7 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
     a.list = nullptr;
     a.lookback = nullptr;
     a.epoch = 0;
-    if (G <= kSplitWgMaxChunks && codec != kCodecVbz) {  // the look-back range split
+    if (passes == 1 && G <= kSplitWgMaxChunks && codec != kCodecVbz) {  // the look-back range split (one epoch per pass)
         rc = take_lookback(c, s, a.lookback, a.epoch);
         if (rc) return rc;
     }
@@ -1808,11 +1847,12 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
             HIPCHK(hipEventRecord(c->evStage[b], c->side));
             HIPCHK(hipStreamWaitEvent(s, c->evStage[b], 0));
         }
-        if (G <= kSplitWgMaxChunks && (size_t)nu * G <= slots)  // few chunks: a workgroup per stream
+        const bool coop = G <= kSplitWgMaxChunks && (size_t)nu * G <= slots;
+        if (coop)  // few chunks: a workgroup per stream (C5: the frames place themselves, enc_place_frame)
             hipLaunchKernelGGL(enc_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopEncWaves), 0, s, a);
         else hipLaunchKernelGGL(enc_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
-        else hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
+        else if (!(coop && a.lookback)) hipLaunchKernelGGL(enc_assemble_kernel, dim3((unsigned)G), dim3(64), 0, s, a);
         if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], s));
     }
     HIPCHK(hipGetLastError());
@@ -1866,7 +1906,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.list = nullptr;
     a.lookback = nullptr;
     a.epoch = 0;
-    if (G <= kMergeWgMaxChunks && codec != kCodecVbz && !c->diagNoMerge) {  // the look-back range merge
+    if (passes == 1 && G <= kMergeWgMaxChunks && codec != kCodecVbz && !c->diagNoMerge) {  // the look-back range merge (one epoch per pass)
         const int lrc = take_lookback(c, s, a.lookback, a.epoch);
         if (lrc) return lrc;
     }

@@ -40,6 +40,11 @@ struct alignas(16) EncLds {
         };
         struct {  // literals; members grouped by lifetime so that each phase's scratch overlays the last
             uint32_t hist2[2][256];  // per-segment histograms, two 16-bit counts per word (histogram -> stream sizes)
+            union {
+            // the odd lanes' copy of hist2 while the histogram is counted (one word further on, so a
+            // byte value counted by both halves of the wave lands in two banks); folded into hist2
+            uint32_t hist2x[1 + 2 * 256];
+            struct {
             uint8_t nbBits[256];  // tree -> stream sizes
             uint16_t val[256];
             union {
@@ -68,6 +73,8 @@ struct alignas(16) EncLds {
                     uint32_t win[kWinWords];  // output bit window
                     uint32_t cw[256];         // Huffman code | nbBits << 16 (stream sizes -> encode)
                 };
+            };
+            };
             };
         };
         struct {  // sequences section (after the literals section is written)
@@ -1495,7 +1502,10 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     const bool single = n < 256;
     const uint32_t segSize = single ? n : (n + 3) / 4;
     const int nseg = single ? 1 : 4;
-    for (int i = lane; i < 2 * 256; i += 64) (&L.hist2[0][0])[i] = 0;
+    for (int i = lane; i < 2 * 256; i += 64) {
+        (&L.hist2[0][0])[i] = 0;
+        L.hist2x[1 + i] = 0;
+    }
     wave_sync();
     if (COOP && !single) {  // the four segments' histograms on the four waves
         if (lane == 0) {
@@ -1530,7 +1540,7 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
             const uint32_t sa = i / segSize;
             const uint32_t boundary = (sa + 1) * segSize;
             if (i + 16 <= n && i + 16 <= boundary) {  // the usual case: 16 bytes of one segment
-                uint32_t* h = &L.hist2[sa >> 1][0];
+                uint32_t* h = ((lane & 1) ? &L.hist2x[1] : &L.hist2[0][0]) + 256 * (sa >> 1);
                 const uint32_t inc = 1u << (16 * (sa & 1));
 #pragma unroll
                 for (int k = 0; k < 16; k++) atomicAdd(h + ((wd[k >> 2] >> (8 * (k & 3))) & 0xFFu), inc);
@@ -1552,7 +1562,9 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         int s = lane + 64 * q;
-        const uint32_t h01 = L.hist2[0][s], h23 = L.hist2[1][s];
+        const uint32_t h01 = L.hist2[0][s] + L.hist2x[1 + s], h23 = L.hist2[1][s] + L.hist2x[1 + 256 + s];
+        L.hist2[0][s] = h01;
+        L.hist2[1][s] = h23;
         c[q] = (h01 & 0xFFFFu) + (h01 >> 16) + (h23 & 0xFFFFu) + (h23 >> 16);
         L.count[s] = c[q];
         if (c[q]) myMaxSym = (uint32_t)s;
