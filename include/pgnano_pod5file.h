@@ -107,6 +107,21 @@ int pgn_pod5_write_file(const char *path, const pgn_pod5_file *source, int signa
                         const uint8_t *read_ids, const uint32_t *samples, const uint64_t *offsets, const uint8_t *data,
                         uint32_t rows_per_batch, const char *software, const uint8_t *section_marker);
 
+/* The layout pgn_pod5_write_file gives the same arguments, with the signal bytes left zero so that
+ * other processes can write them in place: row_positions[i] (rows entries, may be NULL) receives the
+ * file offset of row i's signal bytes.  write = 0 only computes the positions (path may be NULL);
+ * every process that calls it with the same arguments gets the same positions.  Used by the
+ * multi-GPU copy: rank 0 writes the file, every rank writes its own rows at their positions, so
+ * only sizes cross the collective.  section_marker must be given when the positions are used (the
+ * marker does not move them, but a random one would make the ranks' files differ). */
+int pgn_pod5_write_file_reserved(const char *path, const pgn_pod5_file *source, int signal_type, uint64_t rows,
+                                 const uint8_t *read_ids, const uint32_t *samples, const uint64_t *offsets,
+                                 uint32_t rows_per_batch, const char *software, const uint8_t *section_marker,
+                                 int write, uint64_t *row_positions);
+
+/* The row count of every signal record batch (counts: one entry per batch). */
+int pgn_pod5_signal_batch_row_counts(const pgn_pod5_file *f, uint64_t *counts);
+
 typedef struct pgn_pod5_transcode_stats {
     uint64_t rows;
     uint64_t samples;

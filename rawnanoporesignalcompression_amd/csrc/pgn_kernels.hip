@@ -96,12 +96,8 @@ __host__ __device__ inline EncLayout enc_layout()
 }
 
 struct DecLayout {
-    size_t lit, seqs, tables, htab, seg, bytes;
+    size_t lit, seqs, tables, htab, bytes;
 };
-// segment regions of the one-pass Huffman decoder: (all literal bits) / (shortest code) bytes, so a
-// full 128 KiB block whose average code is up to 2.5x its shortest (a wider one decodes one lane per
-// stream straight into place)
-constexpr size_t kSegScratch = (size_t)320 << 10;
 __host__ __device__ inline DecLayout dec_layout()
 {
     DecLayout l{};
@@ -111,7 +107,6 @@ __host__ __device__ inline DecLayout dec_layout()
     l.seqs = take(12 * (size_t)kMaxDecSeq);
     l.tables = take(4 * ((size_t)kSeqTab + 4));
     l.htab = take(2u << z1::kHufTableLogMax);
-    l.seg = take(kSegScratch);
     l.bytes = o;
     return l;
 }
@@ -324,8 +319,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void en
 }
 
 // The small-batch C5 encode places its frames itself (no enc_assemble_kernel): frame s publishes
-// its size in look-back word 3 s + 2 of its chunk, waits for the sizes of frames 0 .. s-1 (lower
-// workgroups, dispatched first), and copies itself behind their length prefixes (C5.hpp:429-462)
+// its size in look-back word 3 s + 2 of its chunk, waits for the sizes of frames 0 .. s-1, and
+// copies itself behind their length prefixes (C5.hpp:429-462).  enc_zstd_coop_kernel numbers its
+// workgroups u = s * G + g (blob order, coop_unit_stream), so every frame it waits for belongs to a
+// lower-numbered workgroup, which the dispatcher started first: forward progress does not depend on
+// all of a call's workgroups being resident at once (another context or process may hold CUs)
 // when it fits the capacity.  Frame 4 then knows the total and writes the status, the size and the
 // stats as enc_assemble_kernel does.  On DST_TOO_SMALL the bytes that fit may have been written
 // (as in the fused kernel, which writes its frames straight into the blob).
@@ -361,6 +359,11 @@ __device__ __noinline__ void enc_place_frame(const EncArgs& a, size_t g, int s, 
     }
 }
 
+// Stream of unit u in the cooperative kernels: blob order (keys, S, M, Llow, Lhigh).  Not the large-
+// first order of the persistent kernels: every workgroup of a cooperative launch starts at once, and
+// enc_place_frame's waits must point at lower-numbered workgroups.
+__device__ __forceinline__ int coop_unit_stream(uint32_t k) { return (int)k; }
+
 // Small batches (the per-chunk calls): one workgroup of kCoopEncWaves waves per stream.  Wave 0
 // compresses the stream; the histograms and the bit packing of its four-segment literals sections
 // are shared with the other waves, one segment each (pgn_zenc.h CoopEncCmd).  A lone chunk's encode
@@ -372,7 +375,7 @@ __global__ __launch_bounds__(64 * kCoopEncWaves) void enc_zstd_coop_kernel(EncAr
     const size_t G = a.G;
     const uint32_t u = blockIdx.x;
     if ((size_t)u >= (size_t)a.nu * G) return;
-    const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
+    const int s = a.nu == 1 ? 0 : coop_unit_stream((uint32_t)(u / G));
     const size_t g = u % G;
     if (a.base + g >= a.nchunks) return;
     if (a.sizes[g * kStreams] == ~0u) return;  // unsupported chunk (the same for every wave)
@@ -485,8 +488,6 @@ struct DecArgs {
     uint64_t* prof;
     size_t base, G;
     uint32_t nu;         // zstd work units per chunk: 5 (C5) or 1 (VBZ)
-    uint32_t segCap;     // Huffman segment scratch per slot; 0 = the two-pass decoder (PGN_HUF=twopass)
-    uint32_t segDiag;    // PGN_SEG_DIAG (timing experiments)
     uint32_t capN;       // fused kernels: as EncArgs
     const uint32_t* list;
     uint64_t* lookback;  // small batches: the range merge's published counts / sums / results (kMergeRanges x 3 per chunk)
@@ -548,11 +549,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     S.maxSeq = kMaxDecSeq;
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
-    S.seg = sbase + lay.seg;
     S.coopCmd = nullptr;
     S.coopStg = nullptr;
-    S.segCap = a.segCap;
-    S.segDiag = a.segDiag;
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = (size_t)a.nu * G;
@@ -640,11 +638,6 @@ __global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs 
     S.maxSeq = kMaxDecSeq;
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
-    S.seg = sbase + lay.seg;
-    S.coopCmd = nullptr;
-    S.coopStg = nullptr;
-    S.segCap = 0;
-    S.segDiag = 0;
     S.coopCmd = cmd;
     S.coopStg = stg;
     const uint64_t dsrc = myUnit.src;
@@ -1175,11 +1168,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.maxSeq = kMaxDecSeq;
     S.tables = (uint32_t*)(sbase + lay.tables);
     S.htab = (uint16_t*)(sbase + lay.htab);
-    S.seg = sbase + lay.seg;
     S.coopCmd = nullptr;
     S.coopStg = nullptr;
-    S.segCap = a.segCap;
-    S.segDiag = a.segDiag;
     uint8_t* inter = sbase + lay.bytes;
     const uint32_t capN = a.capN;
     PhaseProf P;
@@ -1356,9 +1346,6 @@ struct pgn_ctx {
     size_t encStagedBelow = 0;
     size_t encFusedSlotsMax = 0, decFusedSlotsMax = 0;
     size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH, staged pipeline)
-    uint32_t hufSegCap = 0;  // the one-pass Huffman decoder (PGN_HUF=seg) or the two-pass one (0, default)
-    uint32_t segDiag = 0;    // PGN_SEG_DIAG: timing experiments on the one-pass decoder (wrong output)
-    bool diagNoMerge = false;  // PGN_DIAG_NO_MERGE: decode without the merge kernel (timing only, wrong output)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
@@ -1407,10 +1394,14 @@ struct pgn_ctx {
     uint32_t* largeHdrHost = nullptr;
     hipStream_t scanStream = nullptr;
     hipEvent_t evScanFork = nullptr, evScan = nullptr;
+    // the encode and the decode of the large pass keep separate slot scratch: the encoder's hash
+    // tables persist across calls (epoch tags), so a decode must never write over them
     uint8_t* largeScratch = nullptr;
     size_t largeScratchBytes = 0;
     uint32_t* largeEpochs = nullptr;
     size_t largeEpochSlots = 0;
+    uint8_t* largeDecScratch = nullptr;
+    size_t largeDecScratchBytes = 0;
     std::mutex mu;
 };
 
@@ -1495,9 +1486,6 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         c->encForced = true;
     }
     if (const char* pp = getenv("PGN_DEC_PIPELINE")) c->decStaged = strcmp(pp, "staged") == 0;
-    if (const char* dg = getenv("PGN_SEG_DIAG")) c->segDiag = (uint32_t)atoi(dg);
-    if (const char* nm = getenv("PGN_DIAG_NO_MERGE")) c->diagNoMerge = atoi(nm) != 0;
-    if (const char* h = getenv("PGN_HUF")) c->hufSegCap = strcmp(h, "seg") == 0 ? (uint32_t)kSegScratch : 0u;
     if (const char* sb = getenv("PGN_SUBBATCH")) {
         long v = atol(sb);
         if (v > 0) c->subBatch = (size_t)v;
@@ -1555,6 +1543,7 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->largeHdr);
     (void)hipFree(c->largeScratch);
     (void)hipFree(c->largeEpochs);
+    (void)hipFree(c->largeDecScratch);
     if (c->largeHdrHost) (void)hipHostFree(c->largeHdrHost);
     for (hipEvent_t e : {c->evScanFork, c->evScan})
         if (e) (void)hipEventDestroy(e);
@@ -1748,8 +1737,6 @@ static int launch_decode_fused(pgn_ctx* c, int codec, size_t nchunks, const uint
     a.slotBytes = dec_slot_bytes();
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.queue = c->qCur;
-    a.segCap = c->hufSegCap;
-    a.segDiag = c->segDiag;
     a.capN = kPassSamples;
     a.list = nullptr;
     c->lastUnits = nullptr;
@@ -1900,13 +1887,11 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.G = G;
     a.nu = nu;
-    a.segCap = c->hufSegCap;
-    a.segDiag = c->segDiag;
     a.capN = kPassSamples;
     a.list = nullptr;
     a.lookback = nullptr;
     a.epoch = 0;
-    if (passes == 1 && G <= kMergeWgMaxChunks && codec != kCodecVbz && !c->diagNoMerge) {  // the look-back range merge (one epoch per pass)
+    if (passes == 1 && G <= kMergeWgMaxChunks && codec != kCodecVbz) {  // the look-back range merge (one epoch per pass)
         const int lrc = take_lookback(c, s, a.lookback, a.epoch);
         if (lrc) return lrc;
     }
@@ -1922,7 +1907,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         a.base = p * G;
         a.queue = c->qCur + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(s, c->evFree[b], 0));
-        const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots && !c->hufSegCap;
+        const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots;
         a.coopParse = (coop && codec != kCodecVbz) ? 1u : 0u;
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         else if (!a.coopParse) hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
@@ -1933,8 +1918,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
             HIPCHK(hipEventRecord(c->evStage[b], s));
             HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
         }
-        if (c->diagNoMerge) {
-        } else if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         else if (a.lookback)  // few chunks: kMergeRanges single-wave workgroups per chunk
             hipLaunchKernelGGL(dec_merge_lb_kernel, dim3((unsigned)(G * kMergeRanges)), dim3(64), 0, sideS, a);
         else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
@@ -1988,7 +1972,7 @@ static uint32_t large_cap(uint32_t maxN)
     const uint64_t r = ((uint64_t)maxN + 65535u) & ~(uint64_t)65535u;
     return r > PGN_MAX_CHUNK_SAMPLES ? PGN_MAX_CHUNK_SAMPLES : (uint32_t)r;
 }
-static int ensure_large(pgn_ctx* c, size_t bytes, size_t epochSlots)
+static int ensure_large_enc(pgn_ctx* c, size_t bytes, size_t epochSlots)
 {
     if (bytes > c->largeScratchBytes || epochSlots > c->largeEpochSlots) {
         wait_last_host(c);
@@ -2005,6 +1989,18 @@ static int ensure_large(pgn_ctx* c, size_t bytes, size_t epochSlots)
         HIPCHK(hipStreamSynchronize(c->stream));
         c->largeScratchBytes = bytes;
         c->largeEpochSlots = epochSlots;
+    }
+    return PGN_OK;
+}
+static int ensure_large_dec(pgn_ctx* c, size_t bytes)
+{
+    if (bytes > c->largeDecScratchBytes) {
+        wait_last_host(c);
+        (void)hipFree(c->largeDecScratch);
+        c->largeDecScratch = nullptr;
+        c->largeDecScratchBytes = 0;
+        HIPCHK(hipMalloc(&c->largeDecScratch, bytes));
+        c->largeDecScratchBytes = bytes;
     }
     return PGN_OK;
 }
@@ -2032,7 +2028,7 @@ static int launch_large_encode(pgn_ctx* c, int codec, uint32_t count, uint32_t m
     const uint32_t capN = large_cap(maxN);
     const size_t sb = enc_slot_bytes(capN);
     const size_t slots = large_slots(c, count, sb, c->encFusedSlotsMax);
-    int rc = ensure_large(c, sb * slots, slots);
+    int rc = ensure_large_enc(c, sb * slots, slots);
     if (rc) return rc;
     HIPCHK(hipMemsetAsync(c->largeHdr + 2, 0, sizeof(uint32_t), s));
     EncArgs a{};
@@ -2065,7 +2061,7 @@ static int launch_large_decode(pgn_ctx* c, int codec, uint32_t count, uint32_t m
     const uint32_t capN = large_cap(maxN);
     const size_t sb = dec_slot_bytes(capN);
     const size_t slots = large_slots(c, count, sb, c->decFusedSlotsMax);
-    int rc = ensure_large(c, sb * slots, 0);
+    int rc = ensure_large_dec(c, sb * slots);
     if (rc) return rc;
     HIPCHK(hipMemsetAsync(c->largeHdr + 2, 0, sizeof(uint32_t), s));
     DecArgs a{};
@@ -2077,12 +2073,10 @@ static int launch_large_decode(pgn_ctx* c, int codec, uint32_t count, uint32_t m
     a.sampleOffsets = d_sample_offsets;
     a.sampleCounts = d_sample_counts;
     a.status = d_status;
-    a.slotScratch = c->largeScratch;
+    a.slotScratch = c->largeDecScratch;
     a.slotBytes = sb;
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.queue = c->largeHdr + 2;
-    a.segCap = c->hufSegCap;
-    a.segDiag = c->segDiag;
     a.capN = capN;
     a.list = c->largeList;
     return launch_dec_chunks(codec, a, slots, s);

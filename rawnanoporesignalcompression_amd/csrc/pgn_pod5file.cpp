@@ -702,9 +702,12 @@ int32_t put_message(Out& o, const std::vector<uint8_t>& fbm)
 
 // the signal table as an Arrow IPC file (MakeFileWriter + write_batch every rows_per_batch rows,
 // signal_table_writer.cpp:280-330,404-450)
+// data == nullptr: the signal bytes are left zero (reserved for positioned writes); positions (may be
+// null) receives, per row, the table-relative offset of the row's signal bytes.
 std::vector<uint8_t> write_signal_table(int signal_type, uint64_t rows, const uint8_t* read_ids, const uint32_t* samples,
                                         const uint64_t* offsets, const uint8_t* data, uint32_t rows_per_batch,
-                                        const std::vector<KV>& schema_md, const std::vector<KV>& footer_md)
+                                        const std::vector<KV>& schema_md, const std::vector<KV>& footer_md,
+                                        uint64_t* positions = nullptr)
 {
     Out o;
     o.put(kArrowMagic, 6);
@@ -726,7 +729,8 @@ std::vector<uint8_t> write_signal_table(int signal_type, uint64_t rows, const ui
         std::vector<Piece> pieces = {{nullptr, 0}, {read_ids + 16 * r0, (int64_t)(16 * nr)}, {nullptr, 0},
                                      {offs.data(), (int64_t)(8 * (nr + 1))}};
         if (unc) pieces.push_back({nullptr, 0});
-        pieces.push_back({data + d0, (int64_t)(d1 - d0)});
+        const size_t dataPiece = pieces.size();
+        pieces.push_back({data ? data + d0 : nullptr, (int64_t)(d1 - d0)});
         pieces.push_back({nullptr, 0});
         pieces.push_back({samples + r0, (int64_t)(4 * nr)});
         std::vector<ArrowBuf> bufs;
@@ -751,8 +755,12 @@ std::vector<uint8_t> write_signal_table(int signal_type, uint64_t rows, const ui
         blk.meta_len = put_message(o, FbBuilder::finish(message(kHeaderRecordBatch, rb, at)));
         blk.pad = 0;
         blk.body_len = at;
-        for (const Piece& p : pieces) {
-            if (p.n) o.put(p.p, (size_t)p.n);
+        for (size_t k = 0; k < pieces.size(); k++) {
+            const Piece& p = pieces[k];
+            if (k == dataPiece && positions)
+                for (uint64_t i = 0; i < nr; i++) positions[r0 + i] = (uint64_t)o.b.size() + (offsets[r0 + i] - d0);
+            if (p.n && p.p) o.put(p.p, (size_t)p.n);
+            else if (p.n) o.b.resize(o.b.size() + (size_t)p.n, 0);
             o.pad(8);
         }
         blocks.push_back(blk);
@@ -944,14 +952,23 @@ int pgn_pod5_signal_read_batches(const pgn_pod5_file* f, const uint32_t* batch_i
     return PGN_OK;
 }
 
-int pgn_pod5_write_file(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,
-                        const uint8_t* read_ids, const uint32_t* samples, const uint64_t* offsets, const uint8_t* data,
-                        uint32_t rows_per_batch, const char* software, const uint8_t* section_marker)
+int pgn_pod5_signal_batch_row_counts(const pgn_pod5_file* f, uint64_t* counts)
 {
-    if (!path || (rows && (!read_ids || !samples || !offsets)) || signal_type < PGN_POD5_SIGNAL_UNCOMPRESSED ||
+    if (!f || !counts) return PGN_ERR_INVALID_ARG;
+    for (size_t b = 0; b < f->batches.size(); b++) counts[b] = f->batches[b].rows;
+    return PGN_OK;
+}
+
+// pgn_pod5_write_file and pgn_pod5_write_file_reserved: data == nullptr leaves the signal bytes zero;
+// positions (may be null) receives each row's file offset; write == false only computes positions.
+static int write_file_impl(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,
+                           const uint8_t* read_ids, const uint32_t* samples, const uint64_t* offsets,
+                           const uint8_t* data, uint32_t rows_per_batch, const char* software,
+                           const uint8_t* section_marker, bool write, uint64_t* positions)
+{
+    if ((write && !path) || (rows && (!read_ids || !samples || !offsets)) || signal_type < PGN_POD5_SIGNAL_UNCOMPRESSED ||
         signal_type > PGN_POD5_SIGNAL_PGNANO)
         return PGN_ERR_INVALID_ARG;
-    if (rows && offsets[rows] > offsets[0] && !data) return PGN_ERR_INVALID_ARG;
     for (uint64_t i = 0; i < rows; i++)
         if (offsets[i + 1] < offsets[i] ||
             (signal_type == PGN_POD5_SIGNAL_UNCOMPRESSED && (offsets[i + 1] - offsets[i]) != 2ull * samples[i]))
@@ -992,7 +1009,10 @@ int pgn_pod5_write_file(const char* path, const pgn_pod5_file* source, int signa
         std::vector<Entry> entries;
         {
             const std::vector<uint8_t> st = write_signal_table(signal_type, rows, read_ids, samples, offsets, data,
-                                                               rows_per_batch, schema_md, footer_md);
+                                                               rows_per_batch, schema_md, footer_md, positions);
+            if (positions)
+                for (uint64_t i = 0; i < rows; i++) positions[i] += (uint64_t)o.b.size();
+            if (!write) return (int)PGN_OK;
             entries.push_back({(int64_t)o.b.size(), (int64_t)st.size(), PGN_POD5_CONTENT_SIGNAL});
             o.put(st.data(), st.size());
             o.pad(8);
@@ -1037,6 +1057,24 @@ int pgn_pod5_write_file(const char* path, const pgn_pod5_file* source, int signa
         if (w != o.b.size() || c != 0) throw Pod5Error(PGN_ERR_IO, std::string("cannot write ") + path);
         return (int)PGN_OK;
     });
+}
+
+int pgn_pod5_write_file(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,
+                        const uint8_t* read_ids, const uint32_t* samples, const uint64_t* offsets, const uint8_t* data,
+                        uint32_t rows_per_batch, const char* software, const uint8_t* section_marker)
+{
+    if (rows && offsets && offsets[rows] > offsets[0] && !data) return PGN_ERR_INVALID_ARG;
+    return write_file_impl(path, source, signal_type, rows, read_ids, samples, offsets, data, rows_per_batch, software,
+                           section_marker, true, nullptr);
+}
+
+int pgn_pod5_write_file_reserved(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,
+                                 const uint8_t* read_ids, const uint32_t* samples, const uint64_t* offsets,
+                                 uint32_t rows_per_batch, const char* software, const uint8_t* section_marker,
+                                 int write, uint64_t* row_positions)
+{
+    return write_file_impl(path, source, signal_type, rows, read_ids, samples, offsets, nullptr, rows_per_batch,
+                           software, section_marker, write != 0, row_positions);
 }
 
 }  // extern "C"

@@ -73,9 +73,6 @@ struct DecScratch {
     uint32_t maxSeq;
     uint32_t* tables;       // the three sequence FSE tables of a multi-block frame (kSeqTab + 4 words)
     uint16_t* htab;         // 4096 entries: a 12-bit Huffman table, or the parked LDS table
-    uint8_t* seg;           // segment regions of the one-pass Huffman decoder (pgn_hufseg.h)
-    uint32_t segCap;        // their bytes; 0 selects the two-pass decoder (pgn_huf4.h)
-    uint32_t segDiag;       // diagnostic switches (PGN_SEG_DIAG, timing experiments only; wrong output)
     struct CoopCmd __attribute__((address_space(3)))* coopCmd;  // cooperative decode: the section post
     __attribute__((address_space(3))) uint32_t* coopStg;         // ... and wave 0's staging rows
 };
@@ -514,7 +511,6 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
 }  // namespace pgn
 
 #include "pgn_huf4.h"
-#include "pgn_hufseg.h"
 
 namespace pgn {
 
@@ -935,9 +931,6 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
     S.htab = uni(S.htab);
-    S.seg = uni(S.seg);
-    S.segCap = uni(S.segCap);
-    S.segDiag = uni(S.segDiag);
     P.mark(3);  // the work unit's fetch (queue, unit record) up to here
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
@@ -1082,9 +1075,6 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                             if (COOP)
                                 ok = coop_section(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, S.coopCmd,
                                                   S.coopStg, P);
-                            else if (S.segCap)
-                                ok = huf_seg_decode4_wave(hufTl, hufMinNb, hp, remain, litOut, (uint32_t)rs, jt01, jt2,
-                                                          S.seg, S.segCap, P, S.segDiag);
                             else
                                 ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, P);
                         }

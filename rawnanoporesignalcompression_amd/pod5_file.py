@@ -11,8 +11,9 @@ with the signal column decoded and re-encoded by batched GPU launches.
 * :func:`write_pod5` -- a combined file from signal-table rows, copying the other tables of a source;
 * :func:`transcode_pod5` -- the GPU transcoder (a HIP device is required; there is no CPU path); with a
   ``torch.distributed`` group of several ranks (one per GPU) the record batches are shared
-  round-robin, each rank transcodes its share on its GPU (``pgn_pod5_transcode_part``), rank 0
-  gathers the parts and writes the one output file, byte-identical to the one-rank output.
+  round-robin, each rank transcodes its share on its GPU (``pgn_pod5_transcode_part``), the ranks
+  exchange only row sizes, rank 0 writes the file's layout and every rank writes its own rows in
+  place: one output file, byte-identical to the one-rank output.
 """
 from __future__ import annotations
 
@@ -102,6 +103,15 @@ class Pod5File:
             raise Pod5FileError(rc, f"read {self.path}")
         return ids, samples
 
+    def batch_row_counts(self) -> np.ndarray:
+        """Rows of every signal record batch (uint64, one entry per batch)."""
+        counts = np.zeros(self.batches, np.uint64)
+        if self.batches:
+            rc = self._lib.pgn_pod5_signal_batch_row_counts(self._h, counts.ctypes.data)
+            if rc:
+                raise Pod5FileError(rc, f"batch rows of {self.path}")
+        return counts
+
     def batch_rows(self, batch: int) -> tuple[int, int]:
         """(first row, rows) of signal record batch `batch`."""
         r0, n = C.c_uint64(), C.c_uint64()
@@ -123,8 +133,10 @@ class Pod5File:
         samples = np.empty(n, np.uint32)
         offs = np.empty(n + 1, np.uint64)
         data = np.empty(nbytes.value, np.uint8)
-        self._lib.pgn_pod5_signal_read_batches(self._h, _ptr(ids_arr), ids_arr.size, None, None, None, _ptr(ids),
-                                               _ptr(samples), offs.ctypes.data, _ptr(data))
+        rc = self._lib.pgn_pod5_signal_read_batches(self._h, _ptr(ids_arr), ids_arr.size, None, None, None, _ptr(ids),
+                                                    _ptr(samples), offs.ctypes.data, _ptr(data))
+        if rc:
+            raise Pod5FileError(rc, f"batches {ids_arr.tolist()} of {self.path}")
         return SignalTable(ids, samples, offs, data, self.signal_type)
 
     def close(self) -> None:
@@ -187,9 +199,11 @@ def transcode_pod5(in_path: str, out_path: str, dst: str = "pgnano", variant: st
     With torch.distributed initialised and more than one rank in `group` (default: the world), every
     rank must call this with the same arguments: see :func:`transcode_pod5_ranks`.  `device` defaults
     to 0 (one rank) or LOCAL_RANK (several)."""
-    import torch.distributed as dist
-
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+    try:
+        import torch.distributed as dist
+    except ImportError:  # no torch: one rank (the codec itself needs only the native library)
+        dist = None
+    if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         return transcode_pod5_ranks(in_path, out_path, dst, variant, device, rows_per_batch, codec, group)
     from .codec import PGNanoCodec, PGNanoError
 
@@ -237,13 +251,16 @@ def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", varia
 
     Record batch b of the input's signal table goes to rank b % W (the reference's reader decodes
     whole record batches, signal_table_reader.cpp:294-318; its writer takes whole read batches,
-    c_api.cpp:1104-1110), so the ranks share the file with no data exchange until the end.  Each
-    rank transcodes its batches with one batched decode and one batched encode on its GPU; then the
-    ranks all-gather (status, rows, bytes), rank 0 gathers the packed parts, puts the rows back in
-    record-batch order and writes the file exactly as the one-rank call does.  A failure on any rank
-    raises on every rank.  The payload moves over the group's backend (gloo: host tensors; nccl =
-    RCCL: device tensors on this rank's GPU).  Returns the whole job's stats on every rank
-    (decode_ms / encode_ms: the slowest rank's).  `_part` replaces the GPU share (tests on CPU)."""
+    c_api.cpp:1104-1110), so the ranks share the file with no data exchange.  Each rank transcodes
+    its batches with one batched decode and one batched encode on its GPU.  Then the collectives
+    carry sizes only (BASELINE north_star: RCCL for the size reduction): an all-gather of (status,
+    counts) and one of the rows' compressed sizes.  From them every rank computes the same file
+    layout (pgn_pod5_write_file_reserved); rank 0 writes the file with the signal bytes left zero,
+    and every rank writes its own rows' bytes in place (positioned writes).  The file is byte for
+    byte what the one-rank call writes.  A failure on any rank -- also before the first collective
+    (opening the file, creating the codec) -- raises on every rank, and no rank waits on a collective
+    another rank never reaches.  Returns the whole job's stats on every rank (decode_ms / encode_ms:
+    the slowest rank's).  `_part` replaces the GPU share (tests on CPU)."""
     import os
 
     import torch
@@ -252,28 +269,36 @@ def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", varia
     from .codec import PGNanoError
 
     world, rank = dist.get_world_size(group), dist.get_rank(group)
+    root = dist.get_global_rank(group, 0) if group is not None else 0
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", rank))
-    f = Pod5File(in_path)
-    own = False
+    nccl = dist.get_backend(group) == "nccl"
+    f, own = None, False
+    status, msg, counts, times, offs, data = 0, "", [0, 0, 0, 0], [0.0, 0.0], None, None
     try:
-        mine = list(range(rank, f.batches, world))
-        if _part is None:
-            from .codec import PGNanoCodec
-
-            own = codec is None
-            codec = codec or PGNanoCodec(device)
-            status, payload, counts, times = _native_part(codec, f, mine, dst, variant)
-        else:
-            status, payload, counts, times = _part(f, mine, dst, variant)
-        nccl = dist.get_backend(group) == "nccl"
         dev = torch.device("cuda", device) if nccl else torch.device("cpu")
-        if status:
-            counts, times, nbytes = [0, 0, 0, 0], [0.0, 0.0], 0
-        else:
-            offs, data = payload
-            nbytes = 8 * offs.size + data.size
-        head = torch.tensor([status, nbytes] + counts, dtype=torch.int64, device=dev)
+        # ---- local phase: anything that fails here becomes this rank's status, so that every rank
+        # still reaches the first collective
+        try:
+            f = Pod5File(in_path)
+            mine = list(range(rank, f.batches, world))
+            if _part is None:
+                from .codec import PGNanoCodec
+
+                if codec is None:
+                    codec, own = PGNanoCodec(device), True
+                status, payload, c_, t_ = _native_part(codec, f, mine, dst, variant)
+            else:
+                status, payload, c_, t_ = _part(f, mine, dst, variant)
+            if status:
+                msg = str(payload)
+            else:
+                (offs, data), counts, times = payload, c_, t_
+        except Exception as e:  # noqa: BLE001 -- reported to every rank below
+            status = int(getattr(e, "status", 0) or PGN_ERR_IO)
+            msg = f"{type(e).__name__}: {e}"
+        # ---- sizes 1: status and counts of every rank
+        head = torch.tensor([status] + [int(v) for v in counts], dtype=torch.int64, device=dev)
         heads = [torch.empty_like(head) for _ in range(world)]
         dist.all_gather(heads, head, group=group)
         tm = torch.tensor(times, dtype=torch.float64, device=dev)
@@ -282,59 +307,97 @@ def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", varia
         bad = [(r, int(heads[r, 0])) for r in range(world) if heads[r, 0]]
         if bad:
             r, s = bad[0]
-            raise PGNanoError(s, payload if r == rank else f"rank {r} failed")
-        # rank 0 gathers every part (padded to the largest) and writes the file
-        cap = int(heads[:, 1].max())
-        buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
-        if nbytes:
-            mine_bytes = np.concatenate([offs.view(np.uint8), data])
-            buf[:nbytes] = torch.from_numpy(mine_bytes).to(dev)
-        parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-        dist.gather(buf, parts, dst=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+            raise PGNanoError(s, msg if r == rank else f"rank {r} failed")
+        # ---- sizes 2: the compressed size of every row of every rank (padded to the largest part)
+        nrow = heads[:, 1].astype(np.int64)
+        sz = torch.zeros(int(nrow.max()) if world else 0, dtype=torch.int64, device=dev)
+        if nrow[rank]:
+            sz[:int(nrow[rank])] = torch.from_numpy(np.diff(offs).astype(np.int64)).to(dev)
+        parts = [torch.empty_like(sz) for _ in range(world)]
+        dist.all_gather(parts, sz, group=group)
+        parts = [p.cpu().numpy() for p in parts]
+        # ---- the layout every rank computes the same way: rows back in record-batch order
+        sizes, runs = _merge_sizes(f, parts, nrow, world, rank)
+        offs_all = np.zeros(f.rows + 1, np.uint64)
+        np.cumsum(sizes, out=offs_all[1:])
+        ids, samples = f.row_columns()
+        pos = np.zeros(f.rows, np.uint64)
+        lib = _native.load()
         err = None
         if rank == 0:
-            try:
-                _write_gathered(f, parts, heads, world, out_path, dst, rows_per_batch)
-            except Exception as e:  # every rank learns of it below, instead of waiting in a barrier
-                err = e
+            rc = lib.pgn_pod5_write_file_reserved(str(out_path).encode(), f._h, SIGNAL_TYPES[dst], f.rows, _ptr(ids),
+                                                  _ptr(samples), offs_all.ctypes.data, int(rows_per_batch), None,
+                                                  None, 1, _ptr(pos))
+            if rc:
+                err = Pod5FileError(rc, f"write {out_path}")
+        else:
+            rc = lib.pgn_pod5_write_file_reserved(None, f._h, SIGNAL_TYPES[dst], f.rows, _ptr(ids), _ptr(samples),
+                                                  offs_all.ctypes.data, int(rows_per_batch), None, None, 0, _ptr(pos))
+            if rc:
+                err = Pod5FileError(rc, f"layout of {out_path}")
         flag = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
-        dist.broadcast(flag, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
         if err is not None:
             raise err
         if int(flag.item()):
-            raise Pod5FileError(PGN_ERR_IO, f"rank 0 failed to write {out_path}")
-        tot = heads[:, 2:].sum(axis=0)
+            raise Pod5FileError(PGN_ERR_IO, f"another rank failed to lay out {out_path}")
+        # ---- every rank writes its own rows in place, then all agree that the file is complete
+        try:
+            _write_rows_at(out_path, pos, sizes, runs, offs, data)
+        except OSError as e:
+            err = Pod5FileError(PGN_ERR_IO, f"rank {rank}: positioned write to {out_path}: {e}")
+        flag = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if err is not None:
+            raise err
+        if int(flag.item()):
+            raise Pod5FileError(PGN_ERR_IO, f"another rank failed to write its rows of {out_path}")
+        tot = heads[:, 1:].sum(axis=0)
         return _stats_dict(int(tot[0]), int(tot[1]), int(tot[2]), int(tot[3]), float(tm[0]), float(tm[1]))
     finally:
         if own:
             codec.close()
-        f.close()
+        if f is not None:
+            f.close()
 
 
-def _write_gathered(f: Pod5File, parts, heads, world: int, out_path: str, dst: str, rows_per_batch: int) -> None:
-    """Rank 0: the ranks' parts back in record-batch order, written with the source's other tables."""
-    pieces = []
-    for r in range(world):
-        n = int(heads[r, 2])
-        raw = parts[r][:int(heads[r, 1])].cpu().numpy()
-        po = raw[:8 * (n + 1)].view(np.uint64)
-        pieces.append((po, raw[8 * (n + 1):]))
+def _merge_sizes(f: Pod5File, parts, nrow, world: int, rank: int):
+    """Every row's size in record-batch order from the ranks' size lists, and this rank's rows as
+    (first row of the table, first row of the part, count) runs."""
+    counts = f.batch_row_counts().astype(np.int64)
+    first = np.zeros(counts.size + 1, np.int64)
+    np.cumsum(counts, out=first[1:])
     sizes = np.zeros(f.rows, np.uint64)
-    chunks = []
-    at = [0] * world  # next row of each rank's part
+    at = [0] * world
+    runs = []
     for b in range(f.batches):
-        r = b % world
-        po, pdata = pieces[r]
-        first, n = f.batch_rows(b)
-        lo, hi = at[r], at[r] + n
-        sizes[first:first + n] = np.diff(po[lo:hi + 1])
-        chunks.append(pdata[int(po[lo]):int(po[hi])])
-        at[r] = hi
-    if at != [int(heads[r, 2]) for r in range(world)]:
-        raise Pod5FileError(PGN_ERR_IO, "gathered parts disagree with the record batches' row counts")
-    offs_all = np.zeros(f.rows + 1, np.uint64)
-    np.cumsum(sizes, out=offs_all[1:])
-    data_all = np.concatenate(chunks) if chunks else np.empty(0, np.uint8)
-    ids, samples = f.row_columns()
-    write_pod5(out_path, SignalTable(ids, samples, offs_all, data_all, dst), source=f,
-               rows_per_batch=rows_per_batch)
+        r, n = b % world, int(counts[b])
+        sizes[first[b]:first[b] + n] = parts[r][at[r]:at[r] + n]
+        if r == rank and n:
+            runs.append((int(first[b]), at[r], n))
+        at[r] += n
+    if at != [int(v) for v in nrow]:
+        raise Pod5FileError(PGN_ERR_IO, "the ranks' parts disagree with the record batches' row counts")
+    return sizes, runs
+
+
+def _write_rows_at(path: str, pos, sizes, runs, offs, data) -> None:
+    """This rank's rows at their file positions, one write per stretch that is contiguous in the file."""
+    import os
+
+    fd = os.open(str(path), os.O_WRONLY)
+    try:
+        for row0, p0, n in runs:
+            i = 0
+            while i < n:
+                j = i + 1
+                while j < n and int(pos[row0 + j]) == int(pos[row0 + j - 1]) + int(sizes[row0 + j - 1]):
+                    j += 1
+                lo, hi = int(offs[p0 + i]), int(offs[p0 + j])
+                at, buf = int(pos[row0 + i]), memoryview(data[lo:hi])
+                while buf.nbytes:
+                    w = os.pwrite(fd, buf, at)
+                    buf, at = buf[w:], at + w
+                i = j
+    finally:
+        os.close(fd)

@@ -209,6 +209,13 @@ def _failing_part(f, batch_ids, dst, variant):
     return _oracle_part(f, batch_ids, dst, variant)
 
 
+def _raising_part(f, batch_ids, dst, variant):
+    """A rank whose local phase raises before any collective (as a failing codec or open would)."""
+    if batch_ids and batch_ids[0] == 1:
+        raise RuntimeError("codec creation failed")
+    return _oracle_part(f, batch_ids, dst, variant)
+
+
 def _transcode_worker(rank, world, port, src, out, rpb, fail, q):
     import sys
 
@@ -223,8 +230,8 @@ def _transcode_worker(rank, world, port, src, out, rpb, fail, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        st = Pm.transcode_pod5_ranks(src, out, "pgnano", "C5", rows_per_batch=rpb,
-                                     _part=_failing_part if fail else _oracle_part)
+        part = {False: _oracle_part, True: _failing_part, "raise": _raising_part}[fail]
+        st = Pm.transcode_pod5_ranks(src, out, "pgnano", "C5", rows_per_batch=rpb, _part=part)
         q.put((rank, "ok", st))
     except Exception as e:  # noqa: BLE001 -- reported to the parent
         q.put((rank, "error", f"{type(e).__name__}: {e}"))
@@ -294,3 +301,24 @@ def test_multi_rank_transcode_failure_raises_everywhere(tmp_path):
     assert [r[1] for r in res] == ["error", "error"]
     assert "synthetic failure" in res[1][2] and "rank 1 failed" in res[0][2]
     assert not out.exists()
+
+
+def test_multi_rank_transcode_local_exception_reaches_every_rank(tmp_path):
+    """An exception in one rank's local phase (before any collective) becomes its status: every rank
+    raises instead of waiting in a collective the failed rank never joins."""
+    from _golden import HERE as GOLDEN
+    from rawnanoporesignalcompression_amd import pod5_file as Pm
+
+    src = str(tmp_path / "src.pod5")
+    with Pm.Pod5File(os.path.join(GOLDEN, "multi_fast5_zip_v3.pod5")) as f:
+        Pm.write_pod5(src, f.signal_table(), source=f, rows_per_batch=3)
+    out = tmp_path / "never.pod5"
+    res = _run_transcode(2, src, str(out), rpb=100, fail="raise")
+    assert [r[1] for r in res] == ["error", "error"]
+    assert "codec creation failed" in res[1][2] and "rank 1 failed" in res[0][2]
+    assert not out.exists()
+
+
+def test_multi_rank_transcode_missing_input_raises_everywhere(tmp_path):
+    res = _run_transcode(2, str(tmp_path / "absent.pod5"), str(tmp_path / "o.pod5"), rpb=100)
+    assert [r[1] for r in res] == ["error", "error"]

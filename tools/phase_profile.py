@@ -12,12 +12,9 @@ from rawnanoporesignalcompression_amd import PGNanoCodec
 
 ENC = ["split", "search", "lit_gather", "hist", "sort", "hdr(writeCTable)", "huf_encode", "raw_lit", "seq",
        "frame_finish", "assemble", "tree_merge", "tree_depth", "tree_maxheight", "tree_canon"]
-TWO = os.environ.get("PGN_HUF") != "seg"
 DEC = ["parse/merge_wait", "huf_table", "huf_copy(ph3)", "unit_fetch", "seq_exec(rest)", "raw_copy", "merge",
-       "lit_hdr", "huf_store(passB)"] + (["seq_tables", "seq_bits", "huf_spec(passA)", "huf_sync", "seq_decode",
-                                          "seq_copy", "seq_tail"] if TWO else
-                                         ["seg_sync+walk", "seg_compact", "seg_stage", "seg_singles", "seg_bodies",
-                                          "seg_tail", "seg_epochs"])
+       "lit_hdr", "huf_store(passB)", "seq_tables", "seq_bits", "huf_spec(passA)", "huf_sync", "seq_decode",
+       "seq_copy", "seq_tail"]
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 S = 100000
 c = PGNanoCodec(0)
@@ -39,10 +36,8 @@ for name, lab, arr in (("encode", ENC, buf[:16]), ("decode", DEC, buf[16:])):
         if arr[i]:
             print(f"   {l:18s} {100*arr[i]/tot:6.2f}%  {arr[i]/R/1e3:9.1f} kcyc/chunk")
 
-DCNT = (["huf rounds", "passA overlap iters", "passA bitmap iters", "passA main4 iters", "passA tail iters",
-         "sync iters", "sync iters with walks"] if TWO else
-        ["huf sections", "seg rounds", "seg single iters", "seg body8 iters", "seg tail iters",
-         "seg walk rounds", "-", "seg body4 iters"]) + [
+DCNT = ["huf rounds", "passA overlap iters", "passA bitmap iters", "passA main4 iters", "passA tail iters",
+        "sync iters", "sync iters with walks",
         "passB 1-sym iters", "huf tables", "-", "seq blocks", "blocks", "frames", "raw bytes", "-"]
 print("decode counters per chunk:")
 for i, l in enumerate(DCNT):
