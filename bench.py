@@ -43,6 +43,9 @@ METRIC = "MSamples/s encode+decode (1/2/4/8 GPU) at fixed ratio; % HBM roofline"
 # p_switch in 1/65536 units
 PORES = {"default": 6554, "r941": 7282, "r103": 6554, "r1041": 5243}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+# PMC traffic summaries (tools/traffic.sh) per workload, read into roofline.traffic when their
+# source digest matches the kernels being run
+TRAFFIC_FILES = {"configs[1]": "traffic_r04.json", "configs[4]": "traffic_r04_config4.json"}
 
 
 def parse(argv=None):
@@ -67,7 +70,8 @@ def parse(argv=None):
     p.add_argument("--no-side", action="store_true",
                    help="skip the STREAM-copy, PCIe-inclusive and per-chunk side measurements (profiling runs: "
                         "the kernel statistics then hold only the bench batch's launches)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC traffic summary (default: profiles/ file of this workload, TRAFFIC_FILES)")
     # the other BASELINE configs; the default run is configs[1]
     p.add_argument("--pore", choices=sorted(PORES), default="default",
                    help="generator parameters: dwell per pore chemistry (configs[2] uses r1041)")
@@ -393,15 +397,17 @@ def source_digest() -> str:
     return h.hexdigest()
 
 
-def load_traffic(path, R, S, dominant, applicable):
+def load_traffic(path, R, S, dominant, workload):
     """(bytes per launch of the dominant direction, provenance) from the committed PMC summary, or
-    (None, reason) when it does not apply to this run or was measured on other kernel sources."""
+    (None, reason) when it does not apply to this run (workload: "configs[1]" / "configs[4]", None =
+    no measured file applies) or was measured on other kernel sources."""
     try:
         with open(path) as f:
             tj = json.load(f)
     except (OSError, ValueError):
         return None, f"no traffic file {os.path.relpath(path, ROOT)}"
-    if not applicable or tj.get("reads") != R or tj.get("samples") != S:
+    if (workload is None or tj.get("workload", "configs[1]") != workload or tj.get("reads") != R
+            or tj.get("samples") != S):
         return None, "traffic file measured on another workload"
     if tj.get("source_sha256") != source_digest():
         return None, "stale: traffic file measured on other kernel sources"
@@ -526,8 +532,14 @@ def run_rank(args, rank, world, local, codec, torch, dist, device="cuda", cuda=T
     k_ms = (d_ms if args.decode_only else max(e_ms, d_ms)) / max(len(batches), 1) if batches else 0.0
     algo_bytes = (2.0 + c_per_sample) * R0 * S  # per launch (encode 2 + C, decode C + 2 per sample)
     achieved = algo_bytes / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
-    traffic, traffic_src = load_traffic(args.traffic_json, R0, S, dominant,
-                                        applicable=not (args.mixed_pores or args.pore != "default" or args.decode_only))
+    if args.mixed_pores and args.decode_only:
+        wl = "configs[4]"
+    elif not (args.mixed_pores or args.pore != "default" or args.decode_only):
+        wl = "configs[1]"
+    else:
+        wl = None
+    tpath = args.traffic_json or os.path.join(ROOT, "profiles", TRAFFIC_FILES.get(wl, TRAFFIC_FILES["configs[1]"]))
+    traffic, traffic_src = load_traffic(tpath, R0, S, dominant, wl)
     if args.mixed_pores:
         gen = "configs[4]: mixed pores (thirds R9.4.1 / R10.3 / R10.4.1 generator dwell)"
     elif args.pore != "default":

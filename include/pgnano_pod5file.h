@@ -119,6 +119,29 @@ int pgn_pod5_write_file_reserved(const char *path, const pgn_pod5_file *source, 
                                  uint32_t rows_per_batch, const char *software, const uint8_t *section_marker,
                                  int write, uint64_t *row_positions);
 
+/* Keep-going copy (the reference's `copy` after a failing read, src/c++/copy.cpp:174-176): the rows
+ * whose row_status is not 0 could not be written.  Read batch by read batch of the source's reads
+ * table, read by read: a read's signal rows are written up to its first failing row; that read and
+ * the rest of its read batch are not written (pod5_add_reads_data stops at the failing read,
+ * pod5/c++/pod5_format/c_api.cpp:1118-1127); the rows written before the failing one stay in the
+ * signal table, listed by no read.  The reads table is rewritten with the kept reads and their
+ * signal rows renumbered (its dictionaries and schema copied byte for byte); with no failing row
+ * the file is the one pgn_pod5_write_file writes.  Rows no read lists are written when they
+ * transcoded.  Without a reads table (or source) every failing row is dropped on its own. */
+typedef struct pgn_pod5_keep_going_result {
+    uint64_t failed_batches;    /* read batches cut short */
+    uint64_t dropped_reads;     /* reads not written */
+    uint64_t dropped_rows;      /* signal rows not written */
+    uint64_t orphan_rows;       /* rows written before a failing row of their read (listed by no read) */
+    uint64_t first_failed_row;  /* input signal row of the first failure in read order; UINT64_MAX if none */
+    int32_t first_status;
+    int32_t pad;
+} pgn_pod5_keep_going_result;
+int pgn_pod5_write_file_keep_going(const char *path, const pgn_pod5_file *source, int signal_type, uint64_t rows,
+                                   const uint8_t *read_ids, const uint32_t *samples, const uint64_t *offsets,
+                                   const uint8_t *data, const int32_t *row_status, uint32_t rows_per_batch,
+                                   const uint8_t *section_marker, pgn_pod5_keep_going_result *res);
+
 /* The row count of every signal record batch (counts: one entry per batch). */
 int pgn_pod5_signal_batch_row_counts(const pgn_pod5_file *f, uint64_t *counts);
 
@@ -140,6 +163,16 @@ typedef struct pgn_pod5_transcode_stats {
  * pgn_pod5_last_error, pgnano_pod5.h). */
 int pgn_pod5_transcode_file(pgn_ctx *ctx, const char *in_path, const char *out_path, int dst_signal_type,
                             int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats *stats);
+
+/* pgn_pod5_transcode_file with flags: PGN_POD5_KEEP_GOING -- a row the encoder refuses does not fail
+ * the call; the file is written as the reference's `copy` writes it after a failing read
+ * (pgn_pod5_write_file_keep_going), the outcome in *keep_going (may be NULL).  Rows whose input
+ * does not decode still fail the call (the reference's copy logs them and writes unspecified
+ * signal). */
+#define PGN_POD5_KEEP_GOING 1u
+int pgn_pod5_transcode_file_ex(pgn_ctx *ctx, const char *in_path, const char *out_path, int dst_signal_type,
+                               int pgnano_variant, uint32_t rows_per_batch, uint32_t flags,
+                               pgn_pod5_transcode_stats *stats, pgn_pod5_keep_going_result *keep_going);
 
 /* One rank's share of a multi-GPU `copy` (the reference's writer takes whole read batches,
  * c_api.cpp:1104-1110; its reader decodes record batches, signal_table_reader.cpp:294-318): the

@@ -95,6 +95,10 @@ SIGNATURES = [
     ("pgn_pod5_write_file_reserved", C.c_int, [C.c_char_p, _VP, C.c_int, C.c_uint64, _VP, _VP, _VP, C.c_uint32,
                                                C.c_char_p, _VP, C.c_int, _VP]),
     ("pgn_pod5_signal_batch_row_counts", C.c_int, [_VP, _VP]),
+    ("pgn_pod5_write_file_keep_going", C.c_int, [C.c_char_p, _VP, C.c_int, C.c_uint64, _VP, _VP, _VP, _VP, _VP,
+                                                 C.c_uint32, _VP, _VP]),
+    ("pgn_pod5_transcode_file_ex", C.c_int, [_VP, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                             _VP, _VP]),
     ("pgn_pod5_transcode_file", C.c_int, [_VP, C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_uint32, _VP]),
     ("pgn_pod5_signal_batch_rows", C.c_int, [_VP, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("pgn_pod5_signal_read_batches", C.c_int, [_VP, _VP, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),

@@ -1,0 +1,104 @@
+// pgn_hufjob.h -- deferred four-stream Huffman sections (large decode batches).
+//
+// The frame decoder (zstd_decompress_wave in dec_zstd_kernel) decodes every zstd frame of a pass
+// except the four Huffman streams of a literals-only last block (HUF_decompress4X1 at the call
+// C5.hpp:588-667 makes; on the C5 data these are the M frame and most keys frames, 88 % of a chunk's
+// literals): those it leaves as a job -- the streams' places, the destination and a compact copy of
+// the decode table -- and dec_huf_kernel decodes them afterwards, one LANE per stream, 16 frames per
+// wave, every symbol once from its stream's true start.  The frame decoder's own four-stream path
+// (pgn_huf4.h) splits one stream over 16 lanes and decodes every symbol twice (a speculative pass, a
+// synchronisation, an exact pass); the lane-per-stream decoder has no speculation and no sync, but
+// one lane's stream is ~16k symbols long, so it only pays with thousands of frames in flight
+// (launch_decode_impl uses it for large passes).
+//
+// Compact table (LDS budget: 16 frames x 1 KiB per wave).  zstd's single-symbol table (HUF_readDTableX1)
+// has 2^tl entries; codes longer than K bits are canonical and occupy the low indices [0, T) (weight 1
+// first), codes of at most K bits repeat every entry 2^(tl-K) times above T.  Keeping [0, T) whole and
+// one entry per 2^(tl-K) above it, the entry of a peek p (the stream's next tl bits) is
+//     idx = min(p, (p >> (tl - K)) + Cc),   Cc = T - (T >> (tl - K))
+// (both arguments are monotone in p and cross at T).  K is chosen per table for the smallest size;
+// a table that does not fit 512 entries (never seen on zstd level-1 output: 400-480 on the bench's
+// keys / M frames) is decoded in place by the frame decoder as before.
+#pragma once
+// included by pgn_zdec.h (after the Huffman table builder; sDec, kHufLdsLog)
+
+namespace pgn {
+
+constexpr uint32_t kJobTab = 512;  // compact table entries (16-bit: nbBits | symbol << 8)
+
+struct HufJob {
+    uint64_t hp;      // the section's jump table; stream k starts at hp + 6 + len[0] + .. + len[k-1]
+    uint64_t dst;     // rs literals (stream k: seg = (rs + 3) / 4 of them at dst + k seg; the last rs - 3 seg)
+    uint32_t len[4];  // stream bytes
+    uint32_t rs;
+    uint32_t tl, K, Cc;
+    uint32_t flag;    // 1: pending for dec_huf_kernel (written for every unit of a pass)
+    uint32_t pad[3];
+};
+static_assert(sizeof(HufJob) == 64, "HufJob header");
+constexpr size_t kJobBytes = sizeof(HufJob) + 2 * kJobTab;
+
+// Frame decoder side (wave-uniform): the section at hp (4 streams, jump table jt01 / jt2, table in
+// sDec.tab with log tl) becomes job `job`.  Returns false -- and leaves the section to the caller's
+// in-place decoder, which then reports any corruption -- when the jump table is inconsistent or the
+// compact table exceeds kJobTab entries.
+__device__ __noinline__ bool huf_defer_section(uint8_t* job, unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst,
+                                               uint32_t rs, uint32_t jt01, uint32_t jt2)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    job = uni(job);
+    tl = uni(tl);
+    hp = uni(hp);
+    remain = uni((uint64_t)remain);
+    dst = uni(dst);
+    rs = uni(rs);
+    jt01 = uni(jt01);
+    jt2 = uni(jt2);
+    const uint32_t l1 = jt01 & 0xFFFFu, l2 = jt01 >> 16, l3 = jt2;
+    if ((size_t)l1 + l2 + l3 + 6 > remain) return false;
+    const uint32_t l4 = (uint32_t)(remain - 6 - l1 - l2 - l3);
+    const uint32_t seg = (rs + 3) / 4;
+    if (seg * 3 > rs || tl < 1 || tl > kHufLdsLog) return false;
+    // T_K for K = tl - 1 .. tl - 4: table entries whose code is longer than K bits
+    uint32_t c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+    const uint32_t tsz = 1u << tl;
+    for (uint32_t u = lane; u < tsz; u += 64) {
+        const uint32_t nb = sDec.tab[u] >> 8;
+        c1 += nb + 1 > tl;
+        c2 += nb + 2 > tl;
+        c3 += nb + 3 > tl;
+        c4 += nb + 4 > tl;
+    }
+    const uint32_t T1 = wave_sum(c1), T2 = wave_sum(c2), T3 = wave_sum(c3), T4 = wave_sum(c4);
+    uint32_t K = tl, T = 0, size = tsz;
+    const uint32_t Ts[4] = {T1, T2, T3, T4};
+#pragma unroll
+    for (uint32_t d = 1; d <= 4; d++) {
+        if (d >= tl) break;
+        const uint32_t t = Ts[d - 1], sz = t + ((tsz - t) >> d);
+        if (sz < size) {
+            size = sz;
+            K = tl - d;
+            T = t;
+        }
+    }
+    if (size > kJobTab) return false;
+    const uint32_t d = tl - K;
+    const uint32_t Cc = T - (T >> d);
+    uint16_t* tab = (uint16_t*)(job + sizeof(HufJob));
+    for (uint32_t j = lane; j < size; j += 64) {
+        const uint32_t e = sDec.tab[j < T ? j : (j - Cc) << d];
+        gst<uint16_t>(tab + j, (uint16_t)((e >> 8) | ((e & 0xFFu) << 8)));
+    }
+    HufJob* J = (HufJob*)job;
+    if (lane == 0) {
+        gst<uint64_t>(&J->hp, (uint64_t)hp);
+        gst<uint64_t>(&J->dst, (uint64_t)dst);
+        gst<uint4>(&J->len[0], make_uint4(l1, l2, l3, l4));
+        gst<uint4>(&J->rs, make_uint4(rs, tl, K, Cc));
+        gst<uint32_t>(&J->flag, 1u);
+    }
+    return true;
+}
+
+}  // namespace pgn

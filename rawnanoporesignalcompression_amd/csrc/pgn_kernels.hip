@@ -117,8 +117,8 @@ __host__ __device__ constexpr size_t inter_cap(uint32_t capN) { return (size_t)5
 // intermediate is the frame content plus 16 bytes, and ZSTD_decompress may fill them.
 constexpr size_t kVbzPadding = 16;
 __host__ __device__ constexpr size_t chunk_inter_bytes(uint32_t capN) { return align_up(inter_cap(capN) + 64, 256); }
-constexpr size_t kInterCap = inter_cap(kPassSamples);
-constexpr size_t kChunkInterBytes = chunk_inter_bytes(kPassSamples);
+// per-chunk decode buffers of the two passes in flight (intermediates, records, Huffman jobs)
+constexpr size_t kDecBufferBudget = (size_t)24 << 30;
 
 // Work-unit order of the per-stream kernels: the large streams first (M, S, keys, Llow, Lhigh), so
 // the dynamic queue ends with short units.
@@ -481,7 +481,8 @@ struct DecArgs {
     const uint32_t* sampleCounts;
     int32_t* status;
     DecUnit* units;      // [G][5]
-    uint8_t* inter;      // G * kChunkInterBytes
+    uint8_t* inter;      // G * interStride
+    size_t interStride;  // bytes between chunks' intermediates: chunk_inter_bytes(capN)
     uint8_t* slotScratch;
     size_t slotBytes;
     uint32_t* queue;
@@ -493,10 +494,13 @@ struct DecArgs {
     uint64_t* lookback;  // small batches: the range merge's published counts / sums / results (kMergeRanges x 3 per chunk)
     uint64_t epoch;      // this call's tag in those words (bits 48..63)
     uint32_t coopParse;  // dec_zstd_coop_kernel parses the chunks itself (no dec_parse_kernel launch)
+    uint8_t* jobs;       // [G][5] HufJob records (pgn_hufjob.h): dec_zstd_kernel defers, dec_huf_kernel decodes; null = in place
 };
 
-// one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586)
-__device__ inline int c5_parse_chunk(const uint8_t* in, uint64_t src0, uint64_t len, DecUnit* u)
+// one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586).
+// Frames claiming more content than the intermediate holds (interCap = 5 capN bytes, capN >= every
+// chunk of the call) or a stream above kPassSamples are PGN_ERR_UNSUPPORTED (include/pgnano_hip.h).
+__device__ inline int c5_parse_chunk(const uint8_t* in, uint64_t src0, uint64_t len, DecUnit* u, size_t interCap)
 {
     const uint8_t* src = in + src0;
     uint64_t pos = 0;
@@ -518,12 +522,12 @@ __device__ inline int c5_parse_chunk(const uint8_t* in, uint64_t src0, uint64_t 
         u[s].len = (uint32_t)fl;
         pos += fl;
     }
-    uint32_t off = 0;
+    uint64_t off = 0;
     for (int s = 0; s < kStreams; s++) {
-        if (cs[s] > kPassSamples) return PGN_ERR_UNSUPPORTED;
+        if (cs[s] > kPassSamples || cs[s] > interCap - off) return PGN_ERR_UNSUPPORTED;
         u[s].cs = (uint32_t)cs[s];
-        u[s].interOff = off;
-        off += (uint32_t)cs[s];
+        u[s].interOff = (uint32_t)off;
+        off += cs[s];
     }
     return PGN_OK;
 }
@@ -535,7 +539,8 @@ __global__ __launch_bounds__(64) void dec_parse_kernel(DecArgs a)
     if (g >= a.G || c >= a.nchunks) return;
     // a chunk above kPassSamples is left to the large-chunk pass
     a.status[c] = a.sampleCounts[c] > kPassSamples ? PGN_ERR_UNSUPPORTED
-                                                   : c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], a.units + g * kStreams);
+                                                   : c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], a.units + g * kStreams,
+                                                                    inter_cap(a.capN));
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void dec_zstd_kernel(DecArgs a)
@@ -562,16 +567,236 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
         const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
         const size_t g = u % G;
         const size_t c = a.base + g;
+        S.job = a.jobs ? a.jobs + (g * kStreams + (size_t)s) * kJobBytes : nullptr;
+        if (S.job && lane == 0) gst<uint32_t>(&((HufJob*)S.job)->flag, 0u);  // every unit of the pass: fresh
         if (c >= a.nchunks || a.status[c] != PGN_OK) continue;
         DecUnit& d = a.units[g * kStreams + s];
         // destination capacity: the frame content size (C5.hpp:588-667 sizes each stream's slot
         // exactly); VBZ's intermediate carries svb16's 16 padding bytes (signal_compression.cpp:112-118)
         const size_t cap = a.nu == 1 ? (size_t)d.cs + kVbzPadding : (size_t)d.cs;
-        const long r = zstd_decompress_wave(a.in + d.src, d.len, a.inter + g * kChunkInterBytes + d.interOff, cap, S, P);
+        const long r = zstd_decompress_wave(a.in + d.src, d.len, a.inter + g * a.interStride + d.interOff, cap, S, P);
         if (lane == 0) d.dres = (int32_t)r;
         wave_sync();
     }
     P.flush();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deferred four-stream Huffman sections (pgn_hufjob.h): one lane per stream, kHufFrames frames per
+// wave (lane 4f + k: stream k of frame f).  The wave takes the frames of one stream type (M, keys,
+// ...) of kHufFrames consecutive chunks, so its lanes' streams have the same length.  The compact
+// tables go to LDS; a lane reads its stream backwards through a 16-dword LDS ring ([slot][lane],
+// conflict-free) that it refills 16 bytes at a time from global memory one group ahead, and keeps a
+// 64-bit left-aligned bit container: a symbol is a peek of the top bits, the compact-table read, a
+// 64-bit shift by the code length (the entry's low byte) and the symbol byte packed four to a word;
+// every second symbol the container takes the next dword when it holds 32 bits or fewer (a code is
+// at most 11 bits, so two symbols always fit).  Words leave as aligned dword stores (the lane's
+// destination has any alignment: each store joins two words with v_alignbyte; the head and tail
+// bytes are byte stores).  After its symbols a stream must end exactly at its first bit (the strict
+// rule of huf_decode4_wave), else the frame's result is kDecErrHufStream.
+// ---------------------------------------------------------------------------------------------
+constexpr int kHufFrames = 16;
+constexpr uint32_t kRing = 16;  // dwords per lane
+
+__device__ __forceinline__ uint64_t shl64(uint64_t c, uint32_t e)  // c << (e & 63), one v_lshlrev_b64
+{
+    uint64_t r;
+    asm volatile("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "v"(e), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t cnd(bool c, uint32_t a, uint32_t b)  // c ? a : b, one v_cndmask
+{
+    uint32_t r;
+    asm volatile("v_cndmask_b32 %0, %2, %1, %3" : "=v"(r) : "v"(a), "v"(b), "s"((uint64_t)ballot(c)));
+    return r;
+}
+__device__ __forceinline__ uint32_t pick4(bool q1, bool q2, uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    return cnd(q2, cnd(q1, d, c), cnd(q1, b, a));
+}
+__device__ __forceinline__ uint32_t sel4(const uint4& v, uint32_t i)
+{
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+__global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
+{
+    __shared__ __attribute__((aligned(16))) uint16_t tabs[kHufFrames * kJobTab];
+    __shared__ uint32_t ring[kRing * 64];
+    const uint32_t lane = (uint32_t)lane_id();
+    const size_t G = a.G;
+    const uint32_t ngrp = (uint32_t)((G + kHufFrames - 1) / kHufFrames);
+    const uint32_t kq = blockIdx.x / ngrp;  // queue position: the large streams' groups first
+    if (kq >= a.nu) return;
+    const int s = unit_stream(kq);
+    const size_t g0 = (size_t)(blockIdx.x % ngrp) * kHufFrames;
+    const uint32_t f = lane >> 2, q = lane & 3;
+    const size_t g = g0 + f;
+    const bool inb = g < G && a.base + g < a.nchunks;
+    const HufJob* J = (const HufJob*)(a.jobs + (inb ? (g * kStreams + (size_t)s) * kJobBytes : 0));
+    const uint32_t flag = inb ? gld<uint32_t>(&J->flag) : 0u;
+    const uint64_t fm = ballot(flag != 0);
+    if (fm == 0) return;
+    // the pending frames' compact tables (1 KiB each, 16 bytes per lane; all loads in flight at once)
+    {
+        uint4 tv[kHufFrames];
+#pragma unroll
+        for (int ff = 0; ff < kHufFrames; ff++) {
+            const size_t gf = (fm >> (4 * ff)) & 1u ? g0 + (size_t)ff : g0;
+            tv[ff] = gld<uint4>(a.jobs + (gf * kStreams + (size_t)s) * kJobBytes + sizeof(HufJob) + 16 * lane);
+        }
+#pragma unroll
+        for (int ff = 0; ff < kHufFrames; ff++) *(uint4*)&tabs[ff * kJobTab + 8 * lane] = tv[ff];
+    }
+    // this lane's stream
+    uint64_t hp = 0, dstp = 0;
+    uint4 len = make_uint4(0, 0, 0, 0), prm = make_uint4(0, 11, 11, 0);
+    if (flag) {
+        hp = gld<uint64_t>(&J->hp);
+        dstp = gld<uint64_t>(&J->dst);
+        len = gld<uint4>(&J->len[0]);
+        prm = gld<uint4>(&J->rs);
+    }
+    const uint32_t rs = prm.x, tl = prm.y, K = prm.z, Cc = prm.w;
+    const uint32_t so = (q > 0 ? len.x : 0u) + (q > 1 ? len.y : 0u) + (q > 2 ? len.z : 0u);
+    const uint32_t sl = sel4(len, q);
+    const uint32_t seg = (rs + 3) / 4;
+    uint32_t nsym = flag ? (q == 3 ? rs - 3 * seg : seg) : 0u;
+    const uint8_t* src = (const uint8_t*)hp + 6 + so;
+    uint8_t* sdst = (uint8_t*)dstp + (size_t)seg * q;
+    const uint32_t lastB = (flag && sl) ? (uint32_t)gb(src + sl - 1) : 0u;
+    bool bad = flag && lastB == 0;
+    if (bad) nsym = 0;
+    const uint32_t sh1 = 32 - tl, sh2 = 32 - K;
+    const uint32_t tbase = f * kJobTab;
+    uint32_t* rl = ring + lane;  // slot t of this lane: rl[64 t]
+    // ---- bit reader: the top dword (holding the end marker) into the container, the rest of its
+    // 16-byte block and the next three blocks into the ring, two more blocks in registers (staged a
+    // super-group later, so their loads have 16 symbols' time to arrive)
+    const uint64_t e = (uint64_t)src + (sl ? sl - 1 : 0);
+    const uint64_t amin = (uint64_t)src & ~(uint64_t)15;  // reads stay in blocks holding stream bytes
+    uint64_t gaddr = e & ~(uint64_t)15;
+    const uint32_t hb = lastB ? z1::highbit32(lastB) : 0u;
+    const uint32_t i0 = (uint32_t)(e >> 2) & 3u;
+    const uint32_t v0 = (uint32_t)(e & 3u) * 8u + hb;  // valid bits of the top dword
+    const uint32_t totalBits = sl ? (sl - 1) * 8u + hb : 0u;
+    uint64_t C = 0;
+    uint32_t avail = 0, ins = 0, wpos = 0, nd = 0;
+    uint4 Ga = make_uint4(0, 0, 0, 0), Gb = Ga;
+    auto stage = [&](const uint4& blk) {  // a block's dwords, highest address first
+        rl[64 * (wpos & (kRing - 1))] = blk.w;
+        rl[64 * ((wpos + 1) & (kRing - 1))] = blk.z;
+        rl[64 * ((wpos + 2) & (kRing - 1))] = blk.y;
+        rl[64 * ((wpos + 3) & (kRing - 1))] = blk.x;
+        wpos += 4;
+    };
+    auto next_block = [&]() { gaddr = gaddr - 16 >= amin ? gaddr - 16 : amin; return gld<uint4>((const void*)gaddr); };
+    if (nsym || (flag && !bad)) {
+        const uint4 b0 = gld<uint4>((const void*)gaddr);
+        const uint4 b1 = next_block();
+        const uint4 b2 = next_block();
+        const uint4 b3 = next_block();
+        Ga = next_block();
+        Gb = next_block();
+        const uint32_t dw0 = sel4(b0, i0);
+        C = v0 ? ((uint64_t)dw0 << (64 - v0)) : 0ull;
+        avail = v0;
+        if (i0 >= 1) rl[0] = sel4(b0, i0 - 1);
+        if (i0 >= 2) rl[64] = sel4(b0, i0 - 2);
+        if (i0 >= 3) rl[128] = sel4(b0, 0);
+        wpos = i0;
+        stage(b1);
+        stage(b2);
+        stage(b3);
+        // first refill (avail <= 31)
+        nd = rl[0];
+        C |= (uint64_t)nd << (32 - avail);
+        avail += 32;
+        ins = 1;
+        nd = rl[64];
+    }
+    auto refill = [&]() {
+        const bool m = avail <= 32;
+        const uint32_t x = m ? nd : 0u;
+        C |= shl64((uint64_t)x, 32u - avail);
+        avail += m ? 32u : 0u;
+        ins += m ? 1u : 0u;
+        nd = rl[64 * (ins & (kRing - 1))];
+    };
+    auto symbol = [&]() -> uint32_t {
+        const uint32_t hi = (uint32_t)(C >> 32);
+        const uint32_t p = hi >> sh1, pq = (hi >> sh2) + Cc;
+        const uint32_t ent = tabs[tbase + (p < pq ? p : pq)];
+        C = shl64(C, ent);
+        avail -= ent & 0xFFu;
+        return ent;
+    };
+    auto word4 = [&]() -> uint32_t {  // four symbols (refill checks after the second and fourth)
+        const uint32_t e0 = symbol();
+        const uint32_t e1 = symbol();
+        refill();
+        const uint32_t e2 = symbol();
+        const uint32_t e3 = symbol();
+        refill();
+        // byte 1 of each entry: the symbol
+        return __builtin_amdgcn_perm(e1, e0, 0x0C0C0501u) | __builtin_amdgcn_perm(e3, e2, 0x05010C0Cu);
+    };
+    // ---- output: super-groups of 16 symbols; aligned 16-byte stores D_j = output bytes
+    // [h + 16 (j - 1), h + 16 j), taken from the previous and the current super-group's words at the
+    // lane's byte offset h (a funnel: dword offset h / 4 by selects, byte offset h % 4 by v_alignbyte)
+    const uint32_t h = (16u - ((uint32_t)(uintptr_t)sdst & 15u)) & 15u;  // head bytes before the first aligned block
+    uint8_t* A0 = sdst + h;
+    const uint32_t rb = h & 3u;
+    const bool q1 = (h >> 2) & 1u, q2 = (h >> 3) & 1u;
+    uint32_t P[4] = {0, 0, 0, 0}, F[4] = {0, 0, 0, 0};
+    const uint32_t sgroups = nsym / 16;
+    const uint32_t maxGroups = wave_max(sgroups);
+    for (uint32_t it = 0; it < maxGroups; it++) {
+        if (it < sgroups) {
+            uint32_t W[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) W[k] = word4();
+            if (wpos - ins <= kRing - 8) {  // room for two blocks: the ones loaded a super-group ago
+                stage(Ga);
+                stage(Gb);
+                Ga = next_block();
+                Gb = next_block();
+            }
+            if (it == 0) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) F[k] = W[k];
+            } else {
+                // X_m = word h / 4 + m of {P, W}: two levels of per-lane selects (no indexed array,
+                // which the compiler would place in scratch)
+                const uint32_t X0 = pick4(q1, q2, P[0], P[1], P[2], P[3]), X1 = pick4(q1, q2, P[1], P[2], P[3], W[0]),
+                               X2 = pick4(q1, q2, P[2], P[3], W[0], W[1]), X3 = pick4(q1, q2, P[3], W[0], W[1], W[2]),
+                               X4 = pick4(q1, q2, W[0], W[1], W[2], W[3]);
+                gst<uint4>(A0 + 16 * (it - 1), make_uint4(__builtin_amdgcn_alignbyte(X1, X0, rb),
+                                                          __builtin_amdgcn_alignbyte(X2, X1, rb),
+                                                          __builtin_amdgcn_alignbyte(X3, X2, rb),
+                                                          __builtin_amdgcn_alignbyte(X4, X3, rb)));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) P[k] = W[k];
+        }
+    }
+    // the head bytes (in the first super-group) and the pending bytes of the last one
+    if (sgroups) {
+        for (uint32_t b = 0; b < h; b++) gst<uint8_t>(sdst + b, (uint8_t)(sel4(make_uint4(F[0], F[1], F[2], F[3]), b >> 2) >> (8 * (b & 3))));
+        const uint32_t J16 = 16 * sgroups - 16;  // first symbol of the last super-group
+        for (uint32_t b = h; b < 16; b++)
+            gst<uint8_t>(sdst + J16 + b, (uint8_t)(sel4(make_uint4(P[0], P[1], P[2], P[3]), b >> 2) >> (8 * (b & 3))));
+    }
+    // the remaining symbols one by one
+    for (uint32_t i = 16 * sgroups; i < nsym; i++) {
+        const uint32_t ent = symbol();
+        refill();
+        gst<uint8_t>(sdst + i, (uint8_t)(ent >> 8));
+    }
+    // exact end: the stream's bits consumed to its first bit
+    if (flag && !bad) bad = (v0 + 32u * ins - avail) != totalBits;
+    const uint64_t bm = ballot(bad);
+    if (q == 0 && flag && ((bm >> (4 * f)) & 0xFull)) gst<int32_t>(&a.units[g * kStreams + (size_t)s].dres, (int32_t)z1::kDecErrHufStream);
 }
 
 // Small batches (the per-chunk calls): one workgroup of kCoopWaves waves per work unit.  Wave 0
@@ -596,7 +821,8 @@ __global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs 
         if (threadIdx.x == 0) {
             DecUnit uu[kStreams];
             const int rc = a.sampleCounts[c] > kPassSamples ? PGN_ERR_UNSUPPORTED
-                                                            : c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], uu);
+                                                            : c5_parse_chunk(a.in, a.inOffsets[c], a.inSizes[c], uu,
+                                                                             inter_cap(a.capN));
             parseRc = rc;
             if (rc == PGN_OK) myUnit = uu[s];
             if (s == 0) {  // the chunk's first frame publishes its status and frame records for the merge
@@ -640,10 +866,11 @@ __global__ __launch_bounds__(64 * kCoopWaves) void dec_zstd_coop_kernel(DecArgs 
     S.htab = (uint16_t*)(sbase + lay.htab);
     S.coopCmd = cmd;
     S.coopStg = stg;
+    S.job = nullptr;
     const uint64_t dsrc = myUnit.src;
     const uint32_t dlen = myUnit.len, dcs = myUnit.cs, doff = myUnit.interOff;
     const size_t cap = a.nu == 1 ? (size_t)dcs + kVbzPadding : (size_t)dcs;
-    const long r = zstd_decompress_wave<true>(a.in + dsrc, dlen, a.inter + g * kChunkInterBytes + doff, cap, S, P);
+    const long r = zstd_decompress_wave<true>(a.in + dsrc, dlen, a.inter + g * a.interStride + doff, cap, S, P);
     if (lane == 0) a.units[g * kStreams + s].dres = (int32_t)r;
     coop_finish(cmd);
     P.flush();
@@ -667,7 +894,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void de
     }
     if (st == PGN_OK) {
         uint64_t consumed = 0;
-        const int bad = c5_merge_wave(a.inter + g * kChunkInterBytes, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres,
+        const int bad = c5_merge_wave(a.inter + g * a.interStride, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres,
                                       (uint64_t)d[3].dres, a.samples + a.sampleOffsets[c], a.sampleCounts[c], &consumed, W);
         if (bad) st = PGN_ERR_CORRUPT;
         else if (consumed != total) st = PGN_ERR_REMAINING;
@@ -710,7 +937,7 @@ __global__ __launch_bounds__(64) void dec_merge_lb_kernel(DecArgs a)
     uint64_t* lb = a.lookback + g * (3 * kMergeRanges);
     const uint64_t ep = a.epoch;
     const uint32_t n = a.sampleCounts[c];
-    const uint8_t* in = a.inter + g * kChunkInterBytes;
+    const uint8_t* in = a.inter + g * a.interStride;
     int16_t* out = a.samples + a.sampleOffsets[c];
     const uint64_t dS = (uint64_t)d[1].dres, dM = (uint64_t)d[2].dres, dLl = (uint64_t)d[3].dres;
     const uint64_t kl = ((uint64_t)n + 3) / 4;
@@ -825,7 +1052,7 @@ __global__ __launch_bounds__(64) void vbz_parse_kernel(DecArgs a)
     int st = PGN_OK;
     if (a.sampleCounts[c] > kPassSamples) st = PGN_ERR_UNSUPPORTED;  // the large-chunk pass takes it
     else if (!ok) st = PGN_ERR_NOT_ZSTD;
-    else if (cs + kVbzPadding > kInterCap || len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
+    else if (cs + kVbzPadding > inter_cap(a.capN) || len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
     else {
         u->src = src0;
         u->len = (uint32_t)len;
@@ -859,7 +1086,7 @@ __global__ __launch_bounds__(64) void vbz_merge_kernel(DecArgs a)
         if (svb_key_length(n) > d->cs) {  // keys alone run into the padding (or past it)
             st = svb_key_length(n) <= total ? PGN_ERR_REMAINING : PGN_ERR_CORRUPT;
         } else {
-            const int bad = vbz_merge_wave(a.inter + g * kChunkInterBytes, total, a.samples + a.sampleOffsets[c], n,
+            const int bad = vbz_merge_wave(a.inter + g * a.interStride, total, a.samples + a.sampleOffsets[c], n,
                                            &consumed, W);
             if (bad) st = PGN_ERR_CORRUPT;
             else if (consumed != d->cs) st = PGN_ERR_REMAINING;
@@ -1170,6 +1397,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
     S.htab = (uint16_t*)(sbase + lay.htab);
     S.coopCmd = nullptr;
     S.coopStg = nullptr;
+    S.job = nullptr;
     uint8_t* inter = sbase + lay.bytes;
     const uint32_t capN = a.capN;
     PhaseProf P;
@@ -1311,16 +1539,21 @@ __global__ void synth_tasks_kernel(const uint32_t* counts, size_t nreads, uint64
 }
 
 // The chunks above kPassSamples of a batch (their indices, in any order), their count and the
-// largest sample count: hdr = {count, max}, zeroed by the caller.
+// largest sample count among them, and the largest of all: hdr = {count, max large, -, max all},
+// zeroed by the caller.
 __global__ void large_scan_kernel(const uint32_t* counts, size_t n, uint32_t* list, uint32_t* hdr)
 {
+    uint32_t mx = 0;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const uint32_t v = counts[i];
+        mx = v > mx ? v : mx;
         if (v > kPassSamples) {
             list[atomicAdd(hdr, 1u)] = (uint32_t)i;
             atomicMax(hdr + 1, v);
         }
     }
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(hdr + 3, mx);
 }
 
 }  // namespace pgn
@@ -1346,6 +1579,12 @@ struct pgn_ctx {
     size_t encStagedBelow = 0;
     size_t encFusedSlotsMax = 0, decFusedSlotsMax = 0;
     size_t subBatch = 8192;  // chunks per pipeline pass (PGN_SUBBATCH, staged pipeline)
+    // C5 decode batches of at least deferMin chunks defer their four-stream Huffman sections to
+    // dec_huf_kernel (pgn_hufjob.h), in passes of up to deferG chunks: a lane-per-stream decoder
+    // needs thousands of frames in flight (PGN_DEFER_MIN_CHUNKS / PGN_DEFER_G tune both; the output
+    // is the same either way)
+    size_t deferMin = 12288, deferG = 32768;
+    bool lastDeferred = false;  // the last staged C5 decode deferred its Huffman sections (pgn_ctx_kernels)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
     size_t encSlots = 0;
@@ -1355,9 +1594,10 @@ struct pgn_ctx {
     // decode
     uint8_t* decScratch = nullptr;
     size_t decSlots = 0;
-    uint8_t* decChunks = nullptr;  // per buffer: G * kChunkInterBytes + units
-    size_t decG = 0;
+    uint8_t* decChunks = nullptr;  // per buffer: G * interStride + units (+ Huffman jobs)
+    size_t decBytes = 0;
     DecUnit* lastUnits = nullptr;  // decode records of the last pass (diagnostics)
+    size_t lastG = 0;              // ... for this many chunks
     uint32_t* queues = nullptr;    // a ring of work counters, zeroed when it wraps (one per sub-batch pass)
     size_t qNext = 0;              // next unused counter of the ring
     uint32_t* qCur = nullptr;      // the current call's counters
@@ -1490,6 +1730,8 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         long v = atol(sb);
         if (v > 0) c->subBatch = (size_t)v;
     }
+    if (const char* v = getenv("PGN_DEFER_MIN_CHUNKS")) { const long x = atol(v); if (x > 0) c->deferMin = (size_t)x; }
+    if (const char* v = getenv("PGN_DEFER_G")) { const long x = atol(v); if (x > 0) c->deferG = (size_t)x; }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     const char* pe = getenv("PGN_PHASE_PROFILE");
     if (pe && pe[0] == '1') {
@@ -1597,7 +1839,7 @@ static int ensure_enc(pgn_ctx* c, size_t slots, size_t G)
     return PGN_OK;
 }
 
-static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
+static int ensure_dec(pgn_ctx* c, size_t slots, size_t bytes)
 {
     if (slots > c->decSlots) {
         wait_last_host(c);
@@ -1606,13 +1848,13 @@ static int ensure_dec(pgn_ctx* c, size_t slots, size_t G)
         HIPCHK(hipMalloc(&c->decScratch, dec_slot_bytes() * slots));
         c->decSlots = slots;
     }
-    if (G > c->decG) {  // G = chunk capacity over all buffers
+    if (bytes > c->decBytes) {  // the per-chunk buffers of all passes in flight
         wait_last_host(c);
         (void)hipDeviceSynchronize();
         (void)hipFree(c->decChunks);
         c->decChunks = nullptr;
-        HIPCHK(hipMalloc(&c->decChunks, G * (kChunkInterBytes + kStreams * sizeof(DecUnit))));
-        c->decG = G;
+        HIPCHK(hipMalloc(&c->decChunks, bytes));
+        c->decBytes = bytes;
     }
     return PGN_OK;
 }
@@ -1846,21 +2088,39 @@ static int launch_encode_impl(pgn_ctx* c, int codec, size_t nchunks, const int16
     return PGN_OK;
 }
 
+// capCall: every chunk of the call has at most this many samples (a multiple of 4096, at most
+// kPassSamples); the per-chunk intermediates are spaced for it.
 static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
                          const uint64_t* d_in_sizes, int16_t* d_samples, const uint64_t* d_sample_offsets,
-                         const uint32_t* d_sample_counts, int32_t* d_status, void* stream)
+                         const uint32_t* d_sample_counts, int32_t* d_status, void* stream, uint32_t capCall)
 {
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (!c->decStaged || (codec != kCodecC5 && codec != kCodecVbz))
         return launch_decode_fused(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                                    d_sample_counts, d_status, s);
-    const size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
+    // large C5 batches: deferred Huffman sections (dec_huf_kernel), passes of up to deferG chunks
+    // balanced over the batch; otherwise passes of subBatch chunks
+    bool defer = codec == kCodecC5 && nchunks >= c->deferMin;
+    const size_t stride = chunk_inter_bytes(capCall);
+    size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
+    if (defer) {  // up to deferG chunks per pass, and two passes' buffers within kDecBufferBudget
+        size_t gmax = kDecBufferBudget / (2 * (stride + kStreams * (sizeof(DecUnit) + kJobBytes)));
+        gmax = gmax < c->deferG ? gmax : c->deferG;
+        gmax = gmax < c->subBatch ? c->subBatch : gmax;
+        const size_t np = (nchunks + gmax - 1) / gmax;
+        G = (nchunks + np - 1) / np;
+    }
     const size_t passes = (nchunks + G - 1) / G;
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
     const size_t slots = nu * G < c->decSlotsMax ? nu * G : c->decSlotsMax;
+    const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots;  // few chunks: a workgroup per frame
+    defer = defer && !coop;  // the cooperative kernel decodes its sections itself
+    c->lastDeferred = defer;
     const size_t nbuf = passes > 1 ? 2 : 1;
-    int rc = ensure_dec(c, slots, nbuf * G);
+    const size_t unitBytes = align_up(G * kStreams * sizeof(DecUnit), 256);
+    const size_t bufBytes = G * stride + unitBytes + (defer ? G * kStreams * kJobBytes : 0);
+    int rc = ensure_dec(c, slots, nbuf * bufBytes);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[2], s));
     rc = ensure_queues(c, passes, s);
@@ -1872,7 +2132,6 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         HIPCHK(hipEventRecord(c->evFork, s));
         HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
     }
-    const size_t bufBytes = G * (kChunkInterBytes + kStreams * sizeof(DecUnit));
     DecArgs a;
     a.nchunks = nchunks;
     a.in = d_in;
@@ -1887,7 +2146,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     a.prof = c->prof ? c->prof + kPhases : nullptr;
     a.G = G;
     a.nu = nu;
-    a.capN = kPassSamples;
+    a.capN = capCall;
+    a.interStride = stride;
     a.list = nullptr;
     a.lookback = nullptr;
     a.epoch = 0;
@@ -1902,18 +2162,21 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         const int b = (int)(p & 1);
         uint8_t* buf = c->decChunks + (size_t)b * bufBytes;
         a.inter = buf;
-        a.units = (DecUnit*)(buf + G * kChunkInterBytes);
+        a.units = (DecUnit*)(buf + G * stride);
+        a.jobs = defer ? buf + G * stride + unitBytes : nullptr;
         c->lastUnits = a.units;
+        c->lastG = G;
         a.base = p * G;
         a.queue = c->qCur + p;
         if (p >= 2) HIPCHK(hipStreamWaitEvent(s, c->evFree[b], 0));
-        const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots;
         a.coopParse = (coop && codec != kCodecVbz) ? 1u : 0u;
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         else if (!a.coopParse) hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
-        if (coop)  // few chunks: a workgroup per frame
+        if (coop)
             hipLaunchKernelGGL(dec_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopWaves), 0, s, a);
         else hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
+        if (defer)  // the deferred sections: kHufFrames frames of one stream type per wave
+            hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, s, a);
         if (passes > 1) {
             HIPCHK(hipEventRecord(c->evStage[b], s));
             HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
@@ -1953,13 +2216,13 @@ static int start_scan(pgn_ctx* c, size_t nchunks, const uint32_t* d_counts, hipS
     }
     HIPCHK(hipEventRecord(c->evScanFork, s));
     HIPCHK(hipStreamWaitEvent(c->scanStream, c->evScanFork, 0));
-    HIPCHK(hipMemsetAsync(c->largeHdr, 0, 2 * sizeof(uint32_t), c->scanStream));
+    HIPCHK(hipMemsetAsync(c->largeHdr, 0, 4 * sizeof(uint32_t), c->scanStream));
     unsigned grid = (unsigned)((nchunks + 255) / 256);
     grid = grid > 1024 ? 1024 : grid;
     hipLaunchKernelGGL(large_scan_kernel, dim3(grid), dim3(256), 0, c->scanStream, d_counts, nchunks, c->largeList,
                        c->largeHdr);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->largeHdrHost, c->largeHdr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->scanStream));
+    HIPCHK(hipMemcpyAsync(c->largeHdrHost, c->largeHdr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->scanStream));
     HIPCHK(hipEventRecord(c->evScan, c->scanStream));
     return PGN_OK;
 }
@@ -2011,12 +2274,19 @@ static size_t large_slots(pgn_ctx* c, uint32_t count, size_t slotBytes, size_t f
     return slots ? slots : 1;
 }
 
-static int finish_scan(pgn_ctx* c, uint32_t& count, uint32_t& maxN)
+static int finish_scan(pgn_ctx* c, uint32_t& count, uint32_t& maxN, uint32_t* maxAll = nullptr)
 {
     HIPCHK(hipEventSynchronize(c->evScan));
     count = c->largeHdrHost[0];
     maxN = c->largeHdrHost[1];
+    if (maxAll) *maxAll = c->largeHdrHost[3];
     return PGN_OK;
+}
+// the batched decode's per-chunk sample bound: a multiple of 4096 covering every chunk of the call
+static uint32_t call_cap(uint32_t maxN)
+{
+    const uint32_t r = (maxN + 4095u) & ~4095u;
+    return r < 4096u ? 4096u : (r > kPassSamples ? kPassSamples : r);
 }
 
 static int launch_large_encode(pgn_ctx* c, int codec, uint32_t count, uint32_t maxN, size_t nchunks,
@@ -2119,12 +2389,21 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->haveLast) HIPCHK(hipStreamWaitEvent(s, c->evLast, 0));
     const bool scan = need_scan(maxHint);
+    // The intermediates are spaced for the call's largest chunk.  Large C5 batches (the deferred
+    // Huffman path, many chunks per pass) read it from the scan before launching; the others keep
+    // kPassSamples when the caller gives no bound (the scan then runs beside the batched pass).
+    const bool early = scan && codec == kCodecC5 && c->decStaged && nchunks >= c->deferMin;
+    uint32_t capCall = (!scan && maxHint) ? call_cap(maxHint) : kPassSamples;
+    uint32_t count = 0, maxN = 0, maxAll = 0;
     int rc = scan ? start_scan(c, nchunks, d_sample_counts, s) : PGN_OK;
+    if (rc == PGN_OK && early) {
+        rc = finish_scan(c, count, maxN, &maxAll);
+        capCall = call_cap(maxAll);
+    }
     if (rc == PGN_OK)
         rc = launch_decode_impl(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
-                                d_sample_counts, d_status, s);
-    uint32_t count = 0, maxN = 0;
-    if (rc == PGN_OK && scan) rc = finish_scan(c, count, maxN);
+                                d_sample_counts, d_status, s, capCall);
+    if (rc == PGN_OK && scan && !early) rc = finish_scan(c, count, maxN);
     if (rc == PGN_OK && count)
         rc = launch_large_decode(c, codec, count, maxN, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                                  d_sample_counts, d_status, s);
@@ -2298,7 +2577,7 @@ int pgn_debug_phase_cycles(pgn_ctx* c, uint64_t* out, int n)
 int pgn_debug_decode_units(pgn_ctx* c, void* out, size_t nchunks)
 {
     if (!c || !out) return PGN_ERR_INVALID_ARG;
-    if (!c->lastUnits || nchunks > c->decG) return PGN_ERR_INVALID_ARG;
+    if (!c->lastUnits || nchunks > c->lastG) return PGN_ERR_INVALID_ARG;
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, c->lastUnits, nchunks * kStreams * sizeof(DecUnit), hipMemcpyDeviceToHost));
@@ -2310,7 +2589,9 @@ const char* pgn_ctx_kernels(pgn_ctx* c, int direction)
     if (!c) return "";
     if (direction == 0)
         return c->encStaged ? "enc_split_kernel + enc_zstd_kernel + enc_assemble_kernel" : "enc_chunk_kernel<C5>";
-    return c->decStaged ? "dec_parse_kernel + dec_zstd_kernel + dec_merge_kernel" : "dec_chunk_kernel<C5>";
+    if (!c->decStaged) return "dec_chunk_kernel<C5>";
+    return c->lastDeferred ? "dec_parse_kernel + dec_zstd_kernel + dec_huf_kernel + dec_merge_kernel"
+                           : "dec_parse_kernel + dec_zstd_kernel + dec_merge_kernel";
 }
 
 float pgn_ctx_last_encode_ms(pgn_ctx* c)

@@ -640,15 +640,25 @@ int pgn_pod5_decompress_rows(pgn_pod5_batch* b, uint32_t row_count, const uint64
 }
 
 static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
-                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats);
+                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats,
+                          uint32_t flags, pgn_pod5_keep_going_result* kg);
 
 // the host vectors are sized from the file: an allocation failure (or any exception) becomes a
 // status instead of crossing the C ABI
 int pgn_pod5_transcode_file(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
                             int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats)
 {
+    return pgn_pod5_transcode_file_ex(ctx, in_path, out_path, dst_signal_type, pgnano_variant, rows_per_batch, 0,
+                                      stats, nullptr);
+}
+
+int pgn_pod5_transcode_file_ex(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
+                               int pgnano_variant, uint32_t rows_per_batch, uint32_t flags,
+                               pgn_pod5_transcode_stats* stats, pgn_pod5_keep_going_result* keep_going)
+{
     try {
-        return transcode_impl(ctx, in_path, out_path, dst_signal_type, pgnano_variant, rows_per_batch, stats);
+        return transcode_impl(ctx, in_path, out_path, dst_signal_type, pgnano_variant, rows_per_batch, stats, flags,
+                              keep_going);
     } catch (const std::bad_alloc&) {
         snprintf(g_pod5_err, sizeof(g_pod5_err), "out of host memory");
         return PGN_ERR_IO;
@@ -662,11 +672,15 @@ int pgn_pod5_transcode_file(pgn_ctx* ctx, const char* in_path, const char* out_p
 
 // One device pass over a signal column: decode (unless uncompressed), re-encode as dst_signal_type,
 // pack on the device, download the packed column.  outOffs gets n + 1 offsets into outData.
+// encStatus (keep-going): rows the encoder refuses do not fail the call; their statuses come back
+// here (the packed column holds the other rows, a refused row takes no bytes).
 static int transcode_rows(pgn_ctx* ctx, int srcType, int dst_signal_type, int pgnano_variant, size_t n,
                           const std::vector<uint32_t>& samples, const std::vector<uint64_t>& offs,
                           const std::vector<uint8_t>& data, uint64_t dataBytes, uint64_t total,
-                          std::vector<uint64_t>& outOffs, std::vector<uint8_t>& outData, float& decMs, float& encMs)
+                          std::vector<uint64_t>& outOffs, std::vector<uint8_t>& outData, float& decMs, float& encMs,
+                          std::vector<int32_t>* encStatus = nullptr)
 {
+    if (encStatus) encStatus->assign(n, 0);
     outOffs.assign(n + 1, 0);
     outData.clear();
     decMs = encMs = 0;
@@ -768,7 +782,9 @@ static int transcode_rows(pgn_ctx* ctx, int srcType, int dst_signal_type, int pg
         P5CHK(hipMemcpyAsync(&first, d + oFirst, 4, hipMemcpyDeviceToHost, stream));
         P5CHK(hipStreamSynchronize(stream));
         P5CHK(hipEventElapsedTime(&encMs, ev[2], ev[3]));
-        if (first < n) {
+        if (first < n && encStatus) {
+            P5CHK(hipMemcpy(encStatus->data(), d + oStatus, 4 * n, hipMemcpyDeviceToHost));
+        } else if (first < n) {
             int32_t s = 0;
             P5CHK(hipMemcpy(&s, d + oStatus + 4 * (size_t)first, 4, hipMemcpyDeviceToHost));
             snprintf(g_pod5_err, sizeof(g_pod5_err), "row %u: encode status %d", first, s);
@@ -796,7 +812,8 @@ static bool transcode_args_ok(pgn_ctx* ctx, int dst_signal_type, int pgnano_vari
 }
 
 static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_path, int dst_signal_type,
-                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats)
+                          int pgnano_variant, uint32_t rows_per_batch, pgn_pod5_transcode_stats* stats,
+                          uint32_t flags, pgn_pod5_keep_going_result* kg)
 {
     if (!in_path || !out_path || !transcode_args_ok(ctx, dst_signal_type, pgnano_variant)) return PGN_ERR_INVALID_ARG;
     pgn_pod5_file* f = nullptr;
@@ -814,11 +831,21 @@ static int transcode_impl(pgn_ctx* ctx, const char* in_path, const char* out_pat
     std::vector<uint64_t> offs(rows + 1), outOffs;
     pgn_pod5_signal_read(f, ids.data(), samples.data(), offs.data(), data.data());
     float decMs = 0, encMs = 0;
+    const bool keepGoing = (flags & PGN_POD5_KEEP_GOING) != 0;
+    std::vector<int32_t> encStatus;
     rc = transcode_rows(ctx, srcType, dst_signal_type, pgnano_variant, (size_t)rows, samples, offs, data, dataBytes,
-                        total, outOffs, outData, decMs, encMs);
+                        total, outOffs, outData, decMs, encMs, keepGoing ? &encStatus : nullptr);
     if (rc == PGN_OK) {
-        rc = pgn_pod5_write_file(out_path, f, dst_signal_type, rows, ids.data(), samples.data(), outOffs.data(),
-                                 outData.data(), rows_per_batch, nullptr, nullptr);
+        if (keepGoing) {
+            pgn_pod5_keep_going_result r{};
+            rc = pgn_pod5_write_file_keep_going(out_path, f, dst_signal_type, rows, ids.data(), samples.data(),
+                                                outOffs.data(), outData.data(), encStatus.data(), rows_per_batch,
+                                                nullptr, &r);
+            if (kg) *kg = r;
+        } else {
+            rc = pgn_pod5_write_file(out_path, f, dst_signal_type, rows, ids.data(), samples.data(), outOffs.data(),
+                                     outData.data(), rows_per_batch, nullptr, nullptr);
+        }
         if (rc) snprintf(g_pod5_err, sizeof(g_pod5_err), "%s", pgn_pod5_file_error());
     }
     if (rc == PGN_OK && stats) {

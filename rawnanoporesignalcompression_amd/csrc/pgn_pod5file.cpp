@@ -321,7 +321,9 @@ struct ArrowField {
     int32_t int_bits = 0;
     bool int_signed = false;
     int32_t byte_width = 0;
+    int16_t fp_precision = 0;  // FloatingPoint: 0 half, 1 single, 2 double
     bool dictionary = false;
+    int32_t dict_bits = 32;    // dictionary index width (DictionaryEncoding.indexType, default int32)
     std::string ext_name;
     std::vector<ArrowField> children;
 };
@@ -353,9 +355,15 @@ ArrowField parse_field(const FbTable& f, int depth)
             a.int_signed = fb_scalar<uint8_t>(ty, 1, 0) != 0;
         } else if (a.type == AT_FixedSizeBinary) {
             a.byte_width = fb_scalar<int32_t>(ty, 0, 0);
+        } else if (a.type == AT_FloatingPoint) {
+            a.fp_precision = fb_scalar<int16_t>(ty, 0, 0);
         }
     }
     a.dictionary = fb_has(f, 4);
+    if (a.dictionary) {
+        const FbTable de = fb_subtable(f, 4);
+        if (fb_has(de, 1)) a.dict_bits = fb_scalar<int32_t>(fb_subtable(de, 1), 0, 32);
+    }
     const FbVec ch = fb_vector(f, 5, 4);
     for (uint32_t i = 0; i < ch.len; i++) a.children.push_back(parse_field(fb_vec_table(ch, i), depth + 1));
     for (const KV& kv : parse_kv(f, 6))
@@ -781,6 +789,349 @@ std::vector<uint8_t> write_signal_table(int signal_type, uint64_t rows, const ui
     return std::move(o.b);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Row filter over an Arrow IPC file: the reads table of a keep-going copy (the reads the reference's
+// `copy` writes when a read batch fails part-way, src/c++/copy.cpp:174-176, c_api.cpp:1118-1127).
+// The schema message, the dictionary batches and the footer are copied byte for byte (the footer's
+// block offsets and lengths patched in place); every record batch is rewritten with its kept rows,
+// and the values of the list column `signal` (signal-table row indices) are renumbered.
+struct IpcBatchIn {
+    const uint8_t* body;
+    int64_t bodyLen;
+    Bytes meta;
+    size_t nodes, bufs;  // vector starts in meta
+    uint32_t nNodes, nBufs;
+    uint32_t ni = 0, bi = 0;
+    std::pair<int64_t, int64_t> node()
+    {
+        if (ni >= nNodes) corrupt("Arrow record batch has fewer field nodes than its schema");
+        int64_t v[2];
+        memcpy(v, meta.p + nodes + 16 * (size_t)ni++, 16);
+        return {v[0], v[1]};
+    }
+    std::pair<const uint8_t*, int64_t> buf()
+    {
+        if (bi >= nBufs) corrupt("Arrow record batch has fewer buffers than its schema");
+        ArrowBuf b;
+        memcpy(&b, meta.p + bufs + 16 * (size_t)bi++, 16);
+        if (b.offset < 0 || b.length < 0 || b.offset > bodyLen || b.length > bodyLen - b.offset)
+            corrupt("Arrow buffer out of range");
+        return {body + b.offset, b.length};
+    }
+};
+struct IpcBatchOut {
+    std::vector<int64_t> nodes;
+    std::vector<ArrowBuf> bufs;
+    Out body;
+    void put(const void* p, size_t n)
+    {
+        bufs.push_back({(int64_t)body.b.size(), (int64_t)n});
+        if (n) body.put(p, n);
+        body.pad(8);
+    }
+};
+
+int fixed_width(const ArrowField& f)
+{
+    if (f.dictionary) return f.dict_bits / 8;
+    switch (f.type) {
+    case AT_Int: return f.int_bits / 8;
+    case AT_FloatingPoint: return f.fp_precision == 0 ? 2 : (f.fp_precision == 1 ? 4 : 8);
+    case AT_FixedSizeBinary: return f.byte_width;
+    default: return 0;
+    }
+}
+
+bool bit_at(const uint8_t* b, int64_t i) { return (b[i >> 3] >> (i & 7)) & 1; }
+
+// the field's arrays for rows `rows` (ascending) of the input; `remap` renumbers a list's uint64 values
+void filter_field(const ArrowField& f, IpcBatchIn& in, const std::vector<int64_t>& rows, IpcBatchOut& out,
+                  const std::vector<int64_t>* remap)
+{
+    const auto nd = in.node();
+    const int64_t L = nd.first, nulls = nd.second;
+    if (L < 0 || nulls < 0) corrupt("Arrow field node out of range");
+    for (int64_t r : rows)
+        if (r >= L) corrupt("row beyond the Arrow array");
+    const int64_t n = (int64_t)rows.size();
+    if (f.type == AT_Null && !f.dictionary) {
+        out.nodes.push_back(n);
+        out.nodes.push_back(n);
+        return;
+    }
+    // validity
+    const auto vb = in.buf();
+    int64_t newNulls = 0;
+    std::vector<uint8_t> valid;
+    if (nulls > 0) {
+        if (vb.second * 8 < L) corrupt("Arrow validity bitmap too short");
+        valid.assign((size_t)(n + 7) / 8, 0);
+        for (int64_t i = 0; i < n; i++) {
+            if (bit_at(vb.first, rows[i])) valid[i >> 3] |= (uint8_t)(1u << (i & 7));
+            else newNulls++;
+        }
+    }
+    out.nodes.push_back(n);
+    out.nodes.push_back(newNulls);
+    if (newNulls) out.put(valid.data(), valid.size());
+    else out.put(nullptr, 0);
+    const int w = fixed_width(f);
+    if (w > 0) {
+        const auto vals = in.buf();
+        if (vals.second < L * w) corrupt("Arrow values buffer too short");
+        std::vector<uint8_t> v((size_t)(n * w));
+        for (int64_t i = 0; i < n; i++) memcpy(v.data() + i * w, vals.first + rows[i] * w, (size_t)w);
+        out.put(v.data(), v.size());
+        return;
+    }
+    switch (f.type) {
+    case AT_Bool: {
+        const auto vals = in.buf();
+        if (vals.second * 8 < L) corrupt("Arrow bool buffer too short");
+        std::vector<uint8_t> v((size_t)(n + 7) / 8, 0);
+        for (int64_t i = 0; i < n; i++)
+            if (bit_at(vals.first, rows[i])) v[i >> 3] |= (uint8_t)(1u << (i & 7));
+        out.put(v.data(), v.size());
+        return;
+    }
+    case AT_Binary: case AT_Utf8: case AT_LargeBinary: case AT_LargeUtf8:
+    case AT_List: case AT_LargeList: {
+        const bool large = f.type == AT_LargeBinary || f.type == AT_LargeUtf8 || f.type == AT_LargeList;
+        const int ow = large ? 8 : 4;
+        const auto ob = in.buf();
+        if (ob.second < (L + 1) * ow) corrupt("Arrow offsets buffer too short");
+        auto off = [&](int64_t i) -> int64_t {
+            if (large) return ld_i64(ob.first + 8 * i);
+            int32_t v;
+            memcpy(&v, ob.first + 4 * i, 4);
+            return v;
+        };
+        std::vector<uint8_t> no((size_t)((n + 1) * ow));
+        std::vector<int64_t> child;
+        int64_t at = 0;
+        for (int64_t i = 0; i <= n; i++) {
+            if (large) memcpy(no.data() + 8 * i, &at, 8);
+            else {
+                const int32_t v = (int32_t)at;
+                memcpy(no.data() + 4 * i, &v, 4);
+            }
+            if (i == n) break;
+            const int64_t a0 = off(rows[i]), a1 = off(rows[i] + 1);
+            if (a0 < 0 || a1 < a0) corrupt("Arrow offsets not monotonic");
+            for (int64_t k = a0; k < a1; k++) child.push_back(k);
+            at += a1 - a0;
+        }
+        out.put(no.data(), no.size());
+        if (f.type == AT_List || f.type == AT_LargeList) {
+            if (f.children.size() != 1) corrupt("Arrow list without one child");
+            filter_field(f.children[0], in, child, out, remap);
+            if (remap) {  // renumber the child's values (uint64): the last buffer written
+                const ArrowBuf& cb = out.bufs.back();
+                for (int64_t i = 0; i < cb.length / 8; i++) {
+                    uint64_t v;
+                    memcpy(&v, out.body.b.data() + cb.offset + 8 * i, 8);
+                    if (v >= remap->size() || (*remap)[v] < 0) corrupt("a kept read lists a dropped signal row");
+                    const uint64_t nv = (uint64_t)(*remap)[v];
+                    memcpy(out.body.b.data() + cb.offset + 8 * i, &nv, 8);
+                }
+            }
+        } else {
+            const auto db = in.buf();
+            std::vector<uint8_t> d;
+            for (int64_t i = 0; i < n; i++) {
+                const int64_t a0 = off(rows[i]), a1 = off(rows[i] + 1);
+                if (a1 > db.second) corrupt("Arrow data buffer too short");
+                d.insert(d.end(), db.first + a0, db.first + a1);
+            }
+            out.put(d.data(), d.size());
+        }
+        return;
+    }
+    case AT_Struct:
+        for (const ArrowField& c : f.children) filter_field(c, in, rows, out, nullptr);
+        return;
+    default:
+        unsupported("Arrow type id " + std::to_string(f.type) + " in a table to filter");
+    }
+}
+
+struct IpcReader {
+    const uint8_t* a = nullptr;
+    size_t len = 0;
+    std::vector<ArrowField> fields;
+    Bytes footer;
+    FbVec dicts, batches;
+    explicit IpcReader(const uint8_t* p, size_t n) : a(p), len(n)
+    {
+        if (len < 18 || memcmp(a, kArrowMagic, 6) || memcmp(a + len - 6, kArrowMagic, 6))
+            corrupt("table is not an Arrow IPC file");
+        int32_t flen;
+        memcpy(&flen, a + len - 10, 4);
+        if (flen <= 0 || (size_t)flen > len - 18) corrupt("Arrow footer length out of range");
+        footer = Bytes{a + len - 10 - flen, (size_t)flen};
+        const FbTable ft = fb_root(footer);
+        const FbTable schema = fb_subtable(ft, 1);
+        const FbVec fv = fb_vector(schema, 1, 4);
+        for (uint32_t i = 0; i < fv.len; i++) fields.push_back(parse_field(fb_vec_table(fv, i), 0));
+        dicts = fb_vector(ft, 2, sizeof(Block));
+        batches = fb_vector(ft, 3, sizeof(Block));
+    }
+    Block block(const FbVec& v, uint32_t i) const
+    {
+        Block blk;
+        memcpy(&blk, footer.p + v.start + (size_t)i * sizeof(Block), sizeof(Block));
+        if (blk.offset < 8 || blk.meta_len < 8 || blk.body_len < 0 || (uint64_t)blk.offset > len ||
+            (uint64_t)blk.meta_len > len - (uint64_t)blk.offset ||
+            (uint64_t)blk.body_len > len - (uint64_t)blk.offset - (uint64_t)blk.meta_len)
+            corrupt("Arrow block out of range");
+        return blk;
+    }
+    IpcBatchIn batch(const Block& blk) const
+    {
+        const uint8_t* m = a + blk.offset;
+        uint32_t cont;
+        int32_t mlen;
+        memcpy(&cont, m, 4);
+        size_t hdr = 4;
+        if (cont == 0xFFFFFFFFu) {
+            memcpy(&mlen, m + 4, 4);
+            hdr = 8;
+        } else {
+            mlen = (int32_t)cont;
+        }
+        if (mlen <= 0 || (int64_t)hdr + mlen > blk.meta_len) corrupt("Arrow message length out of range");
+        IpcBatchIn in;
+        in.meta = Bytes{m + hdr, (size_t)mlen};
+        const FbTable msg = fb_root(in.meta);
+        if (fb_scalar<uint8_t>(msg, 1, 0) != kHeaderRecordBatch) corrupt("Arrow block is not a record batch");
+        const FbTable rb = fb_subtable(msg, 2);
+        if (fb_has(rb, 3)) unsupported("body-compressed Arrow batches");
+        const FbVec nv = fb_vector(rb, 1, 16), bv = fb_vector(rb, 2, 16);
+        in.nodes = nv.start;
+        in.nNodes = nv.len;
+        in.bufs = bv.start;
+        in.nBufs = bv.len;
+        in.body = a + blk.offset + blk.meta_len;
+        in.bodyLen = blk.body_len;
+        return in;
+    }
+};
+
+// the rows of record batch `blk` of the reads table and each read's signal rows
+void read_signal_lists(const IpcReader& r, const Block& blk, int iSignal, std::vector<std::vector<int64_t>>& lists)
+{
+    IpcBatchIn in = r.batch(blk);
+    lists.clear();
+    for (int c = 0; c < (int)r.fields.size(); c++) {
+        if (c != iSignal) {
+            size_t nodes = 0, buffers = 0;
+            count_layout(r.fields[c], nodes, buffers);
+            in.ni += (uint32_t)nodes;
+            in.bi += (uint32_t)buffers;
+            continue;
+        }
+        const auto nd = in.node();
+        const int64_t L = nd.first;
+        (void)in.buf();  // validity
+        const auto ob = in.buf();
+        const ArrowField& f = r.fields[c];
+        const bool large = f.type == AT_LargeList;
+        if (L < 0 || ob.second < (L + 1) * (large ? 8 : 4)) corrupt("reads.signal offsets too short");
+        (void)in.node();
+        (void)in.buf();  // child validity
+        const auto vb = in.buf();
+        for (int64_t i = 0; i < L; i++) {
+            int64_t a0, a1;
+            if (large) {
+                a0 = ld_i64(ob.first + 8 * i);
+                a1 = ld_i64(ob.first + 8 * i + 8);
+            } else {
+                int32_t x, y;
+                memcpy(&x, ob.first + 4 * i, 4);
+                memcpy(&y, ob.first + 4 * i + 4, 4);
+                a0 = x;
+                a1 = y;
+            }
+            if (a0 < 0 || a1 < a0 || a1 * 8 > vb.second) corrupt("reads.signal offsets out of range");
+            std::vector<int64_t> rowsOf;
+            for (int64_t k = a0; k < a1; k++) rowsOf.push_back(ld_i64(vb.first + 8 * k));
+            lists.push_back(std::move(rowsOf));
+        }
+        return;
+    }
+}
+
+// The reads table with the reads keepRead[i] (reads in file order) and signal rows renumbered.
+std::vector<uint8_t> filter_reads_table(const IpcReader& r, int iSignal, const std::vector<bool>& keepRead,
+                                        const std::vector<int64_t>& remap)
+{
+    // messages in file order: dictionaries (copied) and record batches (rewritten)
+    struct Item {
+        Block blk;
+        bool batch;
+        uint32_t idx;
+    };
+    std::vector<Item> items;
+    for (uint32_t i = 0; i < r.dicts.len; i++) items.push_back({r.block(r.dicts, i), false, i});
+    for (uint32_t i = 0; i < r.batches.len; i++) items.push_back({r.block(r.batches, i), true, i});
+    std::sort(items.begin(), items.end(), [](const Item& x, const Item& y) { return x.blk.offset < y.blk.offset; });
+    const int64_t schemaEnd = items.empty() ? (int64_t)r.len - 10 - (int64_t)r.footer.n - 8 : items[0].blk.offset;
+    Out o;
+    o.put(r.a, (size_t)schemaEnd);  // magic and the schema message
+    std::vector<Block> newDict(r.dicts.len), newBatch(r.batches.len);
+    uint64_t read0 = 0;  // first read (file order) of the next record batch
+    std::vector<Item> byIdx(items);
+    std::sort(byIdx.begin(), byIdx.end(), [](const Item& x, const Item& y) {
+        return x.batch != y.batch ? !x.batch : x.idx < y.idx;
+    });
+    std::vector<uint64_t> firstRead(r.batches.len, 0);
+    for (const Item& it : byIdx)
+        if (it.batch) {
+            firstRead[it.idx] = read0;
+            read0 += (uint64_t)std::max<int64_t>(0, r.batch(it.blk).node().first);
+        }
+    for (const Item& it : items) {
+        if (!it.batch) {
+            Block b = it.blk;
+            b.offset = (int64_t)o.b.size();
+            o.put(r.a + it.blk.offset, (size_t)(it.blk.meta_len + it.blk.body_len));
+            newDict[it.idx] = b;
+            continue;
+        }
+        IpcBatchIn in = r.batch(it.blk);
+        const FbTable rb = fb_subtable(fb_root(in.meta), 2);
+        const int64_t length = fb_scalar<int64_t>(rb, 0, 0);
+        std::vector<int64_t> rows;
+        for (int64_t i = 0; i < length; i++)
+            if (keepRead.at(firstRead[it.idx] + (uint64_t)i)) rows.push_back(i);
+        IpcBatchOut out;
+        for (int c = 0; c < (int)r.fields.size(); c++) filter_field(r.fields[c], in, rows, out, c == iSignal ? &remap : nullptr);
+        if (in.ni != in.nNodes || in.bi != in.nBufs) corrupt("Arrow record batch layout does not match the schema");
+        auto rbo = fb_new_table();
+        fb_add(rbo, 0, 8, (uint64_t)rows.size());
+        fb_add(rbo, 1, fb_new_structs(out.nodes.data(), (uint32_t)(out.nodes.size() / 2), 16, 8));
+        fb_add(rbo, 2, fb_new_structs(out.bufs.data(), (uint32_t)out.bufs.size(), 16, 8));
+        Block b;
+        b.offset = (int64_t)o.b.size();
+        b.meta_len = put_message(o, FbBuilder::finish(message(kHeaderRecordBatch, rbo, (int64_t)out.body.b.size())));
+        b.pad = 0;
+        b.body_len = (int64_t)out.body.b.size();
+        o.put(out.body.b.data(), out.body.b.size());
+        newBatch[it.idx] = b;
+    }
+    const uint32_t eos[2] = {0xFFFFFFFFu, 0};
+    o.put(eos, 8);
+    // the footer, its blocks patched in place (same counts, fixed-size structs)
+    std::vector<uint8_t> ftb(r.footer.p, r.footer.p + r.footer.n);
+    for (uint32_t i = 0; i < r.dicts.len; i++) memcpy(ftb.data() + r.dicts.start + 24 * (size_t)i, &newDict[i], 24);
+    for (uint32_t i = 0; i < r.batches.len; i++) memcpy(ftb.data() + r.batches.start + 24 * (size_t)i, &newBatch[i], 24);
+    o.put(ftb.data(), ftb.size());
+    const int32_t fl = (int32_t)ftb.size();
+    o.put(&fl, 4);
+    o.put(kArrowMagic, 6);
+    return std::move(o.b);
+}
+
 std::string uuid_string(const uint8_t u[16])
 {
     char s[40];
@@ -964,7 +1315,8 @@ int pgn_pod5_signal_batch_row_counts(const pgn_pod5_file* f, uint64_t* counts)
 static int write_file_impl(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,
                            const uint8_t* read_ids, const uint32_t* samples, const uint64_t* offsets,
                            const uint8_t* data, uint32_t rows_per_batch, const char* software,
-                           const uint8_t* section_marker, bool write, uint64_t* positions)
+                           const uint8_t* section_marker, bool write, uint64_t* positions,
+                           const std::vector<uint8_t>* readsTable = nullptr)
 {
     if ((write && !path) || (rows && (!read_ids || !samples || !offsets)) || signal_type < PGN_POD5_SIGNAL_UNCOMPRESSED ||
         signal_type > PGN_POD5_SIGNAL_PGNANO)
@@ -1022,8 +1374,13 @@ static int write_file_impl(const char* path, const pgn_pod5_file* source, int si
             for (size_t i = 0; i < source->embedded.size(); i++) {
                 if ((int)i == source->signal_index) continue;
                 const auto& e = source->embedded[i];
-                entries.push_back({(int64_t)o.b.size(), e.length, e.content_type});
-                o.put(source->raw.data() + e.offset, (size_t)e.length);
+                if (readsTable && e.content_type == PGN_POD5_CONTENT_READS) {  // a keep-going copy's reads
+                    entries.push_back({(int64_t)o.b.size(), (int64_t)readsTable->size(), e.content_type});
+                    o.put(readsTable->data(), readsTable->size());
+                } else {
+                    entries.push_back({(int64_t)o.b.size(), e.length, e.content_type});
+                    o.put(source->raw.data() + e.offset, (size_t)e.length);
+                }
                 o.pad(8);
                 o.put(marker, 16);
             }
@@ -1066,6 +1423,116 @@ int pgn_pod5_write_file(const char* path, const pgn_pod5_file* source, int signa
     if (rows && offsets && offsets[rows] > offsets[0] && !data) return PGN_ERR_INVALID_ARG;
     return write_file_impl(path, source, signal_type, rows, read_ids, samples, offsets, data, rows_per_batch, software,
                            section_marker, true, nullptr);
+}
+
+int pgn_pod5_write_file_keep_going(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,
+                                   const uint8_t* read_ids, const uint32_t* samples, const uint64_t* offsets,
+                                   const uint8_t* data, const int32_t* row_status, uint32_t rows_per_batch,
+                                   const uint8_t* section_marker, pgn_pod5_keep_going_result* res)
+{
+    if (!path || (rows && (!read_ids || !samples || !offsets || !row_status))) return PGN_ERR_INVALID_ARG;
+    return guarded([&] {
+        pgn_pod5_keep_going_result r{0, 0, 0, 0, UINT64_MAX, 0, 0};
+        std::vector<uint8_t> keepRow(rows, 0);
+        std::vector<bool> keepRead;
+        int iSignal = -1;
+        std::unique_ptr<IpcReader> reads;
+        if (source)
+            for (const auto& e : source->embedded)
+                if (e.content_type == PGN_POD5_CONTENT_READS) {
+                    reads.reset(new IpcReader(source->raw.data() + e.offset, (size_t)e.length));
+                    break;
+                }
+        if (reads) {
+            for (size_t i = 0; i < reads->fields.size(); i++)
+                if (reads->fields[i].name == "signal") iSignal = (int)i;
+            if (iSignal < 0 || (reads->fields[iSignal].type != AT_List && reads->fields[iSignal].type != AT_LargeList) ||
+                reads->fields[iSignal].dictionary || reads->fields[iSignal].children.size() != 1 ||
+                reads->fields[iSignal].children[0].type != AT_Int || reads->fields[iSignal].children[0].int_bits != 64)
+                corrupt("reads table: no signal list<uint64> column");
+            // read batch by read batch, read by read: a read's rows are written until the first that
+            // fails; then the read and the rest of its batch are not written (the reference's writer
+            // stops pod5_add_reads_data there, c_api.cpp:1118-1127, and copy continues with the next
+            // batch, copy.cpp:174-176).  The rows written before the failing one stay, listed by no read.
+            std::vector<std::vector<int64_t>> lists;
+            for (uint32_t b = 0; b < reads->batches.len; b++) {
+                read_signal_lists(*reads, reads->block(reads->batches, b), iSignal, lists);
+                bool failed = false;
+                for (const auto& rl : lists) {
+                    if (failed) {
+                        keepRead.push_back(false);
+                        r.dropped_reads++;
+                        continue;
+                    }
+                    bool ok = true;
+                    for (int64_t row : rl) {
+                        if (row < 0 || (uint64_t)row >= rows) corrupt("reads table lists a signal row beyond the table");
+                        if (row_status[row] != 0) {
+                            if (r.first_failed_row == UINT64_MAX) {
+                                r.first_failed_row = (uint64_t)row;
+                                r.first_status = row_status[row];
+                            }
+                            ok = false;
+                            break;
+                        }
+                        if (!keepRow[row]) keepRow[row] = 1;
+                    }
+                    if (!ok) {
+                        // the rows kept so far for this read are orphans
+                        for (int64_t row : rl) {
+                            if (row_status[row] != 0) break;
+                            r.orphan_rows++;
+                        }
+                        failed = true;
+                        r.failed_batches++;
+                        r.dropped_reads++;
+                    }
+                    keepRead.push_back(ok);
+                }
+            }
+            // rows no read lists are written when they transcoded (as the plain transcode writes them)
+            std::vector<uint8_t> listed(rows, 0);
+            for (uint32_t b = 0; b < reads->batches.len; b++) {
+                read_signal_lists(*reads, reads->block(reads->batches, b), iSignal, lists);
+                for (const auto& rl : lists)
+                    for (int64_t row : rl) listed[row] = 1;
+            }
+            for (uint64_t i = 0; i < rows; i++)
+                if (!listed[i] && row_status[i] == 0) keepRow[i] = 1;
+        } else {  // no reads table: every row stands alone
+            for (uint64_t i = 0; i < rows; i++) {
+                keepRow[i] = row_status[i] == 0;
+                if (!keepRow[i] && r.first_failed_row == UINT64_MAX) {
+                    r.first_failed_row = i;
+                    r.first_status = row_status[i];
+                }
+            }
+        }
+        std::vector<int64_t> remap(rows, -1);
+        uint64_t kept = 0;
+        for (uint64_t i = 0; i < rows; i++)
+            if (keepRow[i]) remap[i] = (int64_t)kept++;
+        r.dropped_rows = rows - kept;
+        if (res) *res = r;
+        std::vector<uint8_t> nIds(16 * kept), nData;
+        std::vector<uint32_t> nSamples(kept);
+        std::vector<uint64_t> nOffs(kept + 1, 0);
+        for (uint64_t i = 0, k = 0; i < rows; i++) {
+            if (!keepRow[i]) continue;
+            if (offsets[i + 1] < offsets[i]) return (int)PGN_ERR_INVALID_ARG;
+            memcpy(nIds.data() + 16 * k, read_ids + 16 * i, 16);
+            nSamples[k] = samples[i];
+            nData.insert(nData.end(), data + offsets[i], data + offsets[i + 1]);
+            nOffs[k + 1] = nData.size();
+            k++;
+        }
+        std::vector<uint8_t> newReads;
+        const bool rewrite = reads && kept != rows;
+        if (rewrite) newReads = filter_reads_table(*reads, iSignal, keepRead, remap);
+        return write_file_impl(path, source, signal_type, kept, nIds.data(), nSamples.data(), nOffs.data(),
+                               nData.data(), rows_per_batch ? rows_per_batch : PGN_POD5_DEFAULT_SIGNAL_BATCH_ROWS,
+                               nullptr, section_marker, true, nullptr, rewrite ? &newReads : nullptr);
+    });
 }
 
 int pgn_pod5_write_file_reserved(const char* path, const pgn_pod5_file* source, int signal_type, uint64_t rows,

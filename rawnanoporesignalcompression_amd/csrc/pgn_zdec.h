@@ -73,6 +73,8 @@ struct DecScratch {
     uint32_t maxSeq;
     uint32_t* tables;       // the three sequence FSE tables of a multi-block frame (kSeqTab + 4 words)
     uint16_t* htab;         // 4096 entries: a 12-bit Huffman table, or the parked LDS table
+    uint8_t* job;           // this frame's HufJob record (pgn_hufjob.h): a literals-only last block's
+                            // four Huffman streams are left to dec_huf_kernel; null = decode in place
     struct CoopCmd __attribute__((address_space(3)))* coopCmd;  // cooperative decode: the section post
     __attribute__((address_space(3))) uint32_t* coopStg;         // ... and wave 0's staging rows
 };
@@ -511,6 +513,7 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
 }  // namespace pgn
 
 #include "pgn_huf4.h"
+#include "pgn_hufjob.h"
 
 namespace pgn {
 
@@ -931,6 +934,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     S.maxSeq = uni(S.maxSeq);
     S.tables = uni(S.tables);
     S.htab = uni(S.htab);
+    S.job = uni(S.job);
     P.mark(3);  // the work unit's fetch (queue, unit record) up to here
     size_t ip = 0, op = 0;
     if (srcSize == 0) return z1::kDecErrSrcSmall;
@@ -972,7 +976,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
         bool hufValid = false;  // a Huffman table exists for treeless literals
         bool hufInLds = false;  // ... and is in sDec.tab (tables up to kHufLdsLog)
         bool hufParked = false; // ... and a copy is parked in S.htab
-        unsigned hufTl = 0, hufMinNb = 1;
+        unsigned hufTl = 0;
         SeqState fs;  // frame state of the sequences stage: repeat offsets, table validity
         while (true) {
             if (srcSize - ip < 3) return z1::kDecErrSrcSmall;
@@ -1047,7 +1051,6 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                         if (hsz == 0) return z1::kDecErrHufTable;
                         hufValid = true;
                         hufTl = tlNew;
-                        hufMinNb = mnNew;
                         hufInLds = tlNew <= kHufLdsLog;
                         hufParked = !hufInLds;
                         hp += hsz;
@@ -1075,6 +1078,11 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
                             if (COOP)
                                 ok = coop_section(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, S.coopCmd,
                                                   S.coopStg, P);
+                            else if (S.job && last && noSeq &&
+                                     huf_defer_section(S.job, hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2)) {
+                                ok = true;        // dec_huf_kernel decodes the streams (and reports their errors)
+                                S.job = nullptr;  // one job per unit (a later frame of the unit decodes in place)
+                            }
                             else
                                 ok = huf_decode4_wave(hufTl, hp, remain, litOut, (uint32_t)rs, jt01, jt2, P);
                         }

@@ -179,6 +179,43 @@ def write_pod5(path: str, table: SignalTable, source: Pod5File | None = None, ro
         raise Pod5FileError(rc, f"write {path}")
 
 
+class _KeepGoing(C.Structure):  # pgn_pod5_keep_going_result
+    _fields_ = [("failed_batches", C.c_uint64), ("dropped_reads", C.c_uint64), ("dropped_rows", C.c_uint64),
+                ("orphan_rows", C.c_uint64), ("first_failed_row", C.c_uint64), ("first_status", C.c_int32),
+                ("pad", C.c_int32)]
+
+    def as_dict(self) -> dict:
+        d = {k: int(getattr(self, k)) for k, _ in self._fields_ if k != "pad"}
+        if d["first_failed_row"] == 2**64 - 1:
+            d["first_failed_row"] = None
+        return d
+
+
+def write_pod5_keep_going(path: str, table: SignalTable, row_status, source: Pod5File | None = None,
+                          rows_per_batch: int = 100, section_marker: bytes | None = None) -> dict:
+    """The file the reference's ``copy`` leaves when some rows cannot be written (row_status[i] != 0):
+    read batch by read batch of `source`'s reads table, a read's rows up to its first failing one are
+    written, that read and the rest of its batch are not (include/pgnano_pod5file.h
+    pgn_pod5_write_file_keep_going); returns what was dropped."""
+    lib = _native.load()
+    ids = np.ascontiguousarray(table.read_ids, np.uint8).reshape(-1, 16)
+    samples = np.ascontiguousarray(table.samples, np.uint32)
+    offs = np.ascontiguousarray(table.offsets, np.uint64)
+    data = np.ascontiguousarray(table.data, np.uint8)
+    st = np.ascontiguousarray(row_status, np.int32)
+    if offs.size != samples.size + 1 or ids.shape[0] != samples.size or st.size != samples.size:
+        raise ValueError("read_ids, samples, offsets and row_status disagree on the row count")
+    mk = C.create_string_buffer(bytes(section_marker), 16) if section_marker is not None else None
+    res = _KeepGoing()
+    rc = lib.pgn_pod5_write_file_keep_going(str(path).encode(), source._h if source is not None else None,
+                                            SIGNAL_TYPES[table.signal_type], samples.size, _ptr(ids), _ptr(samples),
+                                            offs.ctypes.data, _ptr(data), _ptr(st), int(rows_per_batch),
+                                            C.cast(mk, C.c_void_p) if mk else None, C.byref(res))
+    if rc:
+        raise Pod5FileError(rc, f"write {path}")
+    return res.as_dict()
+
+
 class _TranscodeStats(C.Structure):
     _fields_ = [("rows", C.c_uint64), ("samples", C.c_uint64), ("in_bytes", C.c_uint64), ("out_bytes", C.c_uint64),
                 ("decode_ms", C.c_float), ("encode_ms", C.c_float)]
@@ -191,19 +228,25 @@ def _stats_dict(rows, samples, in_bytes, out_bytes, decode_ms, encode_ms) -> dic
 
 
 def transcode_pod5(in_path: str, out_path: str, dst: str = "pgnano", variant: str = "C5", device: int | None = None,
-                   rows_per_batch: int = 100, codec=None, group=None) -> dict:
+                   rows_per_batch: int = 100, codec=None, group=None, keep_going: bool = False) -> dict:
     """``copy in.pod5 out.pod5 --pgnano`` (dst="pgnano") or ``--VBZ`` (dst="vbz"), or an uncompressed
     signal table (dst="uncompressed"), on the GPU: one batched decode and one batched encode of every
     row, written with the input's read ids, row order, reads and run-info tables.
 
     With torch.distributed initialised and more than one rank in `group` (default: the world), every
     rank must call this with the same arguments: see :func:`transcode_pod5_ranks`.  `device` defaults
-    to 0 (one rank) or LOCAL_RANK (several)."""
+    to 0 (one rank) or LOCAL_RANK (several).
+
+    keep_going: a row the encoder refuses does not fail the call; the file is written as the
+    reference's ``copy`` leaves it (:func:`write_pod5_keep_going`), and the result carries
+    ``keep_going`` (what was dropped).  One rank only."""
     try:
         import torch.distributed as dist
     except ImportError:  # no torch: one rank (the codec itself needs only the native library)
         dist = None
     if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        if keep_going:
+            raise ValueError("keep_going is a single-rank transcode")
         return transcode_pod5_ranks(in_path, out_path, dst, variant, device, rows_per_batch, codec, group)
     from .codec import PGNanoCodec, PGNanoError
 
@@ -211,11 +254,16 @@ def transcode_pod5(in_path: str, out_path: str, dst: str = "pgnano", variant: st
     c = codec or PGNanoCodec(0 if device is None else device)
     try:
         st = _TranscodeStats()
-        rc = c._lib.pgn_pod5_transcode_file(c._h, str(in_path).encode(), str(out_path).encode(), SIGNAL_TYPES[dst],
-                                            _native.VARIANTS[variant], int(rows_per_batch), C.byref(st))
+        kg = _KeepGoing()
+        rc = c._lib.pgn_pod5_transcode_file_ex(c._h, str(in_path).encode(), str(out_path).encode(), SIGNAL_TYPES[dst],
+                                               _native.VARIANTS[variant], int(rows_per_batch),
+                                               1 if keep_going else 0, C.byref(st), C.byref(kg))
         if rc:
             raise PGNanoError(rc, c._lib.pgn_pod5_last_error().decode())
-        return _stats_dict(st.rows, st.samples, st.in_bytes, st.out_bytes, st.decode_ms, st.encode_ms)
+        out = _stats_dict(st.rows, st.samples, st.in_bytes, st.out_bytes, st.decode_ms, st.encode_ms)
+        if keep_going:
+            out["keep_going"] = kg.as_dict()
+        return out
     finally:
         if own:
             c.close()

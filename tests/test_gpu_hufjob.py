@@ -1,0 +1,169 @@
+"""The deferred four-stream Huffman sections (pgn_hufjob.h: dec_zstd_kernel leaves the literals-only
+last block's streams as jobs, dec_huf_kernel decodes them one lane per stream) against the oracle.
+
+Large decode batches take this path (PGN_DEFER_MIN_CHUNKS, default 12,288 chunks); here a codec is
+made with the threshold at 1 chunk and passes of 96 chunks, so that small batches run it: mixed chunk
+sizes (every alignment of the streams' destinations, short last streams, several passes with both
+buffers), the Huffman stress shapes (1-bit to 11-bit codes), corrupted blobs (statuses equal to the
+oracle's, the known X2-tail divergence of DESIGN §3 aside) and full-size chunks.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dcodec():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rawnanoporesignalcompression_amd import PGNanoCodec
+
+    keys = ("PGN_DEFER_MIN_CHUNKS", "PGN_DEFER_G")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ["PGN_DEFER_MIN_CHUNKS"] = "1"
+    os.environ["PGN_DEFER_G"] = "96"
+    try:
+        c = PGNanoCodec(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    yield c
+    c.close()
+
+
+def _decode(codec, blobs, lens):
+    import torch
+
+    dev = torch.device("cuda", 0)
+    sizes = np.array([len(b) for b in blobs], np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    flat = np.frombuffer(b"".join(bytes(b) for b in blobs), np.uint8).copy()
+    if flat.size == 0:
+        flat = np.zeros(1, np.uint8)
+    counts = np.asarray(lens, np.int32)
+    out, _, st = codec.decompress_batch(torch.from_numpy(flat).to(dev), torch.from_numpy(offs).to(dev),
+                                        torch.from_numpy(sizes).to(dev), torch.from_numpy(counts).to(dev))
+    torch.cuda.synchronize()
+    assert "dec_huf_kernel" in codec.kernels(1)
+    so = np.concatenate([[0], np.cumsum(counts.astype(np.int64))])
+    o = out.cpu().numpy()
+    return [o[so[i]:so[i + 1]] for i in range(len(lens))], st.cpu().numpy()
+
+
+def _reads(seed, lens):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i, n in enumerate(lens):
+        if i % 4 == 3:  # wider deltas: longer codes, more class-3 samples
+            out.append(np.clip(np.cumsum(rng.normal(0, 30 + 40 * (i % 7), int(n))), -32768, 32767).astype(np.int16))
+        else:
+            out.append(O.synth_read(9000 + i, int(n)))
+    return out
+
+
+def test_deferred_decode_mixed_sizes_equal_oracle(dcodec):
+    rng = np.random.default_rng(42)
+    lens = list(rng.integers(1, 102401, 290)) + [0, 1, 3, 255, 256, 257, 1024, 4099, 16385, 65792, 102400]
+    reads = _reads(1, lens)
+    blobs = []
+    for x in reads:
+        rc, b, _ = O.c5_compress(x)
+        assert rc == 0
+        blobs.append(b)
+    got, st = _decode(dcodec, blobs, lens)
+    assert (st == 0).all(), np.nonzero(st)[0][:10]
+    for i, x in enumerate(reads):
+        assert np.array_equal(got[i], x), i
+
+
+def test_deferred_decode_huffman_stress_shapes(dcodec):
+    from test_gpu_parity import _huffman_stress_signals
+
+    pairs = []
+    for _, x in _huffman_stress_signals().items():
+        rc, b, _ = O.c5_compress(x)
+        if rc == 0:
+            pairs.append((b, x))
+    pairs = pairs * 8  # several frames per wave of the same shape; more than 64 chunks (no cooperative path)
+    got, st = _decode(dcodec, [b for b, _ in pairs], [x.size for _, x in pairs])
+    assert (st == 0).all()
+    for i, (_, x) in enumerate(pairs):
+        assert np.array_equal(got[i], x), i
+
+
+def _claims_too_much(blob: bytes, n: int) -> bool:
+    """The frames' content sizes exceed the decoder's documented bound (include/pgnano_hip.h,
+    PGN_ERR_UNSUPPORTED: more than 5 bytes per sample, or a stream above 262,144 bytes)."""
+    import ctypes as C
+    import struct
+
+    m = O.model()
+    pos, tot = 0, 0
+    for s in range(5):
+        if s < 4:
+            if pos + 8 > len(blob):
+                return False
+            fl = struct.unpack_from("<Q", blob, pos)[0]
+            pos += 8
+        else:
+            fl = len(blob) - pos
+        if fl > len(blob) - pos:
+            return False
+        fr = np.frombuffer(blob[pos:pos + fl], np.uint8).copy()
+        cs = m.z1m_content_size(fr.ctypes.data_as(C.c_void_p), C.c_size_t(fl)) if fl else -1
+        if cs < 0:
+            return False
+        if cs > 262144:
+            return True
+        tot += cs
+        pos += fl
+    return tot > 5 * n
+
+
+def test_deferred_decode_corrupted_statuses_equal_oracle(dcodec):
+    rng = np.random.default_rng(7)
+    lens = list(rng.integers(2000, 102401, 160))
+    reads = _reads(2, lens)
+    bad = []
+    for i, x in enumerate(reads):
+        rc, b, _ = O.c5_compress(x)
+        b = bytearray(b)
+        if i % 3 == 0:    # a byte inside the frames (most often a Huffman stream of M)
+            b[int(rng.integers(40, len(b)))] ^= int(rng.integers(1, 256))
+        elif i % 3 == 1:  # a flipped bit near the end of a stream region
+            k = int(rng.integers(len(b) // 2, len(b)))
+            b[k] ^= 1 << int(rng.integers(0, 8))
+        bad.append(bytes(b))
+    got, st = _decode(dcodec, bad, lens)
+    for i, b in enumerate(bad):
+        rc, ref = O.c5_decompress(b, int(lens[i]))
+        if rc == 0 and st[i] == 3 and not O.c5_frames_strictly_valid(b):
+            continue  # libzstd's double-symbol decoder accepts one trailing codeword
+        if st[i] == 9 and _claims_too_much(b, int(lens[i])):
+            continue  # a corrupted frame header claims more content than the documented bound
+        assert st[i] == rc, (i, rc, st[i])
+        if rc == 0:
+            assert np.array_equal(got[i], ref), i
+
+
+def test_deferred_decode_full_size_chunks(dcodec):
+    import torch
+
+    n, k = 100_000, 1536
+    samples, offs, cnt = dcodec.synth_reads(k, n, seed=42)
+    enc = dcodec.compress_batch(samples, offs, cnt)
+    out, _, st = dcodec.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
+    torch.cuda.synchronize()
+    assert "dec_huf_kernel" in dcodec.kernels(1)
+    assert (enc.status == 0).all() and (st == 0).all()
+    assert torch.equal(out, samples)

@@ -224,3 +224,48 @@ def test_transcode_uniform_noise_rows_fail_without_fault(codec, tmp_path):
     with Pod5File(back) as f:
         t = f.signal_table()
         assert t.data.tobytes() == data.tobytes()
+
+
+def test_keep_going_transcode_drops_refused_rows(codec, tmp_path):
+    """keep_going=True (pgn_pod5_transcode_file_ex, PGN_POD5_KEEP_GOING): the rows the C5 encoder
+    refuses are dropped instead of failing the call (no reads table here: each row stands alone);
+    the rows around them are the oracle's blobs."""
+    from rawnanoporesignalcompression_amd.pod5_file import Pod5File, SignalTable, transcode_pod5, write_pod5
+
+    import _oracle as O
+
+    rng = np.random.default_rng(5)
+    xs = [O.synth_read(700 + i, 60000) for i in range(5)]
+    xs += [rng.integers(-32768, 32768, 90000).astype(np.int16) for _ in range(30)]
+    xs += [O.synth_read(800 + i, 50000) for i in range(5)]
+    data = np.concatenate([x.view(np.uint8) for x in xs])
+    offs = np.concatenate([[0], np.cumsum([2 * x.size for x in xs])]).astype(np.uint64)
+    ids = rng.integers(0, 256, (len(xs), 16)).astype(np.uint8)
+    src = str(tmp_path / "noise.pod5")
+    write_pod5(src, SignalTable(ids, np.array([x.size for x in xs], np.uint32), offs, data, "uncompressed"))
+    out = str(tmp_path / "kg.pod5")
+    res = transcode_pod5(src, out, "pgnano", codec=codec, keep_going=True)
+    kg = res["keep_going"]
+    assert kg["dropped_rows"] == 30 and kg["first_failed_row"] == 5 and kg["first_status"] == 1
+    keep = xs[:5] + xs[35:]
+    with Pod5File(out) as f:
+        t = f.signal_table()
+    assert t.rows == 10
+    assert [bytes(t.read_ids[i]) for i in range(10)] == [bytes(ids[i]) for i in list(range(5)) + list(range(35, 40))]
+    for i, x in enumerate(keep):
+        assert t.blob(i) == O.c5_compress(x)[1], i
+
+
+def test_keep_going_transcode_without_failures_is_the_plain_copy(codec, tmp_path):
+    from rawnanoporesignalcompression_amd.pod5_file import transcode_pod5
+
+    a, b = str(tmp_path / "a.pod5"), str(tmp_path / "b.pod5")
+    transcode_pod5(FIXTURE, a, "pgnano", codec=codec)
+    res = transcode_pod5(FIXTURE, b, "pgnano", codec=codec, keep_going=True)
+    assert res["keep_going"]["dropped_rows"] == 0
+
+    def unmarked(p):
+        x = open(p, "rb").read()
+        return x.replace(x[8:24], bytes(16))
+
+    assert unmarked(a) == unmarked(b)

@@ -1,5 +1,7 @@
 """One bench step (encode + decode of R reads x S samples, the bench's buffers and launch sequence)
-for the HBM-traffic passes of tools/traffic.sh.  Run under rocprofv3 --pmc on the GPU box."""
+for the HBM-traffic passes of tools/traffic.sh.  Run under rocprofv3 --pmc on the GPU box.
+A third argument "mixed" generates configs[4]'s corpus (thirds with the R9.4.1 / R10.3 / R10.4.1
+generator dwell, bench.py --mixed-pores); its decode is the measured direction there."""
 import os
 import sys
 
@@ -14,7 +16,13 @@ c = PGNanoCodec(0)
 samples = torch.empty(R * S, dtype=torch.int16, device="cuda")
 counts = torch.full((R,), S, dtype=torch.int32, device="cuda")
 offs = torch.arange(R, dtype=torch.int64, device="cuda") * S
-c.synth_reads(R, S, seed=42, out=samples)
+if len(sys.argv) > 3 and sys.argv[3] == "mixed":  # bench.py PORES, thirds of the batch
+    cuts = [0, R // 3, 2 * R // 3, R]
+    for i, pq in enumerate((7282, 6554, 5243)):
+        a, e = cuts[i], cuts[i + 1]
+        c.synth_reads(e - a, S, seed=42, first_read=a, p_switch_q16=pq, out=samples[a * S:e * S])
+else:
+    c.synth_reads(R, S, seed=42, out=samples)
 caps = torch.clamp(counts.to(torch.int64) * 2 + 26, min=1024)
 boffs = torch.zeros(R, dtype=torch.int64, device="cuda")
 boffs[1:] = torch.cumsum(caps, 0)[:-1]

@@ -12,6 +12,7 @@ import os
 import sys
 
 d, R, S, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+workload = sys.argv[5] if len(sys.argv) > 5 else "configs[1]"
 val = collections.defaultdict(lambda: collections.defaultdict(float))
 calls = collections.defaultdict(lambda: collections.defaultdict(int))
 for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recursive=True):
@@ -21,6 +22,8 @@ for f in glob.glob(os.path.join(d, "*", "**", "*counter_collection.csv"), recurs
         calls[k][r["Counter_Name"]] += 1
 stages = {"c5_encode": ["enc_split_kernel", "enc_zstd_kernel", "enc_assemble_kernel"],
           "c5_decode": ["dec_parse_kernel", "dec_zstd_kernel", "dec_merge_kernel"]}
+if "dec_huf_kernel" in val:  # large batches: the deferred Huffman sections
+    stages["c5_decode"].insert(2, "dec_huf_kernel")
 # the fused per-chunk kernels (the default encode path) stand for their whole direction
 if "enc_chunk_kernel<0>" in val:
     stages["c5_encode"] = ["enc_chunk_kernel<0>"]
@@ -29,7 +32,7 @@ if "dec_chunk_kernel<0>" in val:
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from bench import source_digest  # noqa: E402  (the kernel sources this measurement belongs to)
 
-res = {"reads": R, "samples": S, "unit": "bytes per stage launch (one direction over the whole batch)",
+res = {"reads": R, "samples": S, "workload": workload, "unit": "bytes per stage launch (one direction over the whole batch)",
        "source_sha256": source_digest(),
        "correction": "2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)", "kernels": {}}
 for k, v in val.items():
