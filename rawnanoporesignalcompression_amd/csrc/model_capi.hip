@@ -42,6 +42,38 @@ size_t z1m_sequences(const uint8_t* src, size_t n, uint32_t* out3, size_t maxSeq
     return nb;
 }
 
+// The encoder's no-match certificate (pgn_zenc.h no_match_certificate), serially: 1 when the
+// level-1 search of the single-block frame src[0, n) provably finds no match.
+int z1m_no_match_certificate(const uint8_t* src, size_t n)
+{
+    if (n < 7 || n > kMaxSrc) return 0;
+    const Params p = level1_params(n);
+    const long ilimit = (long)n - 8;
+    const uint32_t slots = 8192 / 4;
+    uint32_t* set = (uint32_t*)calloc(slots, 4);
+    int ok = 1;
+    uint32_t e = 257, k = 0;
+    for (;; k++) {
+        if (k % 64 == 0 && 2 * (k + 64) > slots * 7 / 8) { ok = 0; break; }
+        const long pk = (long)e - 256;
+        e += e >> 7;
+        if (!(pk + 1 < ilimit)) break;
+        const uint64_t v8 = rd64(src + pk);
+        if (rd32(src + pk + 1) == (uint32_t)(v8 >> 16)) { ok = 0; break; }  // repcode (offset 1) at ip0 + 2
+        const uint32_t keys[2] = {((uint32_t)v8 ^ (hash_word(v8, p.hashLog, p.mls) * 0x9E3779B1u)) | 1u,
+                                  ((uint32_t)(v8 >> 8) ^ (hash_word(v8 >> 8, p.hashLog, p.mls) * 0x9E3779B1u)) | 1u};
+        for (int j = 0; j < 2 && ok; j++) {
+            uint32_t s = (uint32_t)(((uint64_t)keys[j] * slots) >> 32);
+            while (set[s] && set[s] != keys[j]) s = s + 1 == slots ? 0 : s + 1;
+            if (set[s] == keys[j]) ok = 0;
+            set[s] = keys[j];
+        }
+        if (!ok) break;
+    }
+    free(set);
+    return ok;
+}
+
 long z1m_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap)
 {
     DecWork* w = (DecWork*)malloc(sizeof(DecWork));

@@ -234,6 +234,75 @@ constexpr VisitChains kVisitChainsHost = make_visit_chains();
 static_assert(kVisitChainsHost.e[0][kChainLen - 65] > (1u << 20) + 512u, "visit chain too short");
 __constant__ VisitChains kVisitChains = make_visit_chains();
 
+// No-match certificate (single-block frames).  Until its first match ZSTD_compressBlock_fast visits
+// a data-independent chain of positions (two per iteration, ip0 and ip0 + 1), tests the repcode at
+// ip0 + 2 and, for each visited position, the table's entry for its hash: the latest visited position
+// with that hash.  So if no iteration's repcode holds and no two visited positions share their hash
+// and their first 4 bytes, the search finds nothing: the block is all literals (nbSeq 0, repeat
+// offsets unchanged), whatever the table holds -- and the table (a frame starts with an empty one,
+// tagged per frame) need not be read or written at all.  The pairs are found with a hash set of the
+// 32-bit keys hash ^ bytes in the codec LDS (the search's own LDS is not yet live); any repcode hit or
+// duplicate key -- a real candidate or a key collision -- returns false and the exact search runs.
+// For noise streams (the C5 S / M / Llow streams) this replaces the search's table round trips, the
+// bulk of the encoder's HBM bytes.
+constexpr uint32_t kCertSlots = kCodecLdsBytes / 4;
+// LDS compare-and-swap of an empty (0) word; returns the word's old value
+__device__ __forceinline__ uint32_t lds_cas(lds_u32* p, uint32_t val)
+{
+    uint32_t e = 0;
+    __hip_atomic_compare_exchange_strong(p, &e, val, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return e;
+}
+__device__ __noinline__ bool no_match_certificate(const uint8_t* __restrict__ src, uint32_t n, unsigned hlog, unsigned mls,
+                                                  uint32_t off1)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    src = uni(src);
+    n = uni(n);
+    hlog = uni(hlog);
+    mls = uni(mls);
+    off1 = uni(off1);
+    lds_u32* set = (lds_u32*)sCodecLds;
+    for (uint32_t i = lane; i < kCertSlots; i += 64) set[i] = 0;
+    lds_sync();
+    const int32_t ilimit = (int32_t)n - 8;
+    const uint32_t* E = kVisitChains.e[1];  // the first block of a frame: ip0 = 1, anchor = 0
+    for (uint32_t ci = 0;; ci += 64) {
+        if (2 * (ci + 64) > kCertSlots * 7 / 8) return false;  // the set would fill up: the exact search decides
+        const int32_t pk = (int32_t)E[ci + lane] - 256;
+        const bool valid = pk + 1 < ilimit;
+        bool bad = false;
+        uint32_t k0 = 0, k1 = 0;
+        if (valid) {
+            const uint64_t v8 = ld64u(src + pk);
+            bad = off1 > 0 && ld32u(src + pk + 2 - (int32_t)off1) == (uint32_t)(v8 >> 16);
+            const uint32_t h0 = z1::hash_word(v8, hlog, mls), h1 = z1::hash_word(v8 >> 8, hlog, mls);
+            k0 = ((uint32_t)v8 ^ (h0 * 0x9E3779B1u)) | 1u;  // 0 marks an empty slot
+            k1 = ((uint32_t)(v8 >> 8) ^ (h1 * 0x9E3779B1u)) | 1u;
+        }
+        if (ballot(bad)) return false;
+        // insert both keys (linear probing, LDS compare-and-swap); an equal key already there: a pair
+        uint32_t s0 = (uint32_t)(((uint64_t)k0 * kCertSlots) >> 32), s1 = (uint32_t)(((uint64_t)k1 * kCertSlots) >> 32);
+        bool d0 = !valid, d1 = !valid, dup = false;
+        while (ballot(!d0 || !d1)) {
+            if (!d0) {
+                const uint32_t old = lds_cas(set + s0, k0);
+                if (old == 0u) d0 = true;
+                else if (old == k0) d0 = dup = true;
+                else s0 = s0 + 1 == kCertSlots ? 0u : s0 + 1;
+            }
+            if (!d1) {
+                const uint32_t old = lds_cas(set + s1, k1);
+                if (old == 0u) d1 = true;
+                else if (old == k1) d1 = dup = true;
+                else s1 = s1 + 1 == kCertSlots ? 0u : s1 + 1;
+            }
+        }
+        if (ballot(dup)) return false;
+        if (ballot(!valid)) return true;  // the chain has left the block
+    }
+}
+
 // Match search (ZSTD_compressBlock_fast, libzstd 1.4.x) speculated over 64 consecutive visits.
 // The visit positions follow a data-independent recurrence until a match is found, so lane k takes
 // visit k of the round: it hashes its two positions, reads the table (entries (tag << 17) | idx,
@@ -251,7 +320,7 @@ struct SearchOut {
 __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ src, uint32_t start, uint32_t end, unsigned hlog,
                                                    unsigned mls, uint32_t* __restrict__ ht, uint32_t tag,
                                                    z1::Seq* __restrict__ seqs, uint32_t rep0, uint32_t rep1, uint32_t idxBits,
-                                                   uint32_t lowIdx, uint32_t maxRep)
+                                                   uint32_t lowIdx, uint32_t maxRep, bool single)
 {
     EncLds& L = sEnc;
     const uint32_t lane = (uint32_t)lane_id();
@@ -277,9 +346,20 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     // (1 for a frame within its window; ZSTD_getLowestPrefixIndex of the block's end above it)
     lowIdx = uni(lowIdx);
     maxRep = uni(maxRep);
+    single = __builtin_amdgcn_readfirstlane((int)single) != 0;
     uint32_t off1 = rep0, off2 = rep1, offSaved = 0;
     if (off2 > maxRep) { offSaved = off2; off2 = 0; }
     if (off1 > maxRep) { offSaved = off1; off1 = 0; }
+    if (single && no_match_certificate(src, end, hlog, mls, off1)) {  // the whole frame is one literals block
+        SearchOut r;
+        r.nbSeq = 0;
+        r.lastLL = end - start;
+        r.rep0 = off1 ? off1 : offSaved;
+        r.rep1 = off2 ? off2 : offSaved;
+        r.rounds = 0;
+        r.candIters = 0;
+        return r;
+    }
     uint32_t nbSeq = 0, rounds = 0, candIters = 0;
     const uint64_t below = (1ull << lane) - 1ull, above = ~below & ~(1ull << lane);
     for (int i = (int)lane; i < kFiltSlots; i += 64) L.filt[i] = 0;  // shares storage with the literal stage
@@ -1830,7 +1910,7 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
             const uint32_t ip0 = start + (start == 0 ? 1u : 0u);
             const SearchOut so = fast_search_wave(src, start, start + bs, p.hashLog, p.mls, S.ht, tag, S.seqs, rep0, rep1,
                                                   ht_idx_bits(n), z1::window_low_index(start + bs, p.windowLog),
-                                                  ip0 + 1u - z1::window_low_index(ip0, p.windowLog));
+                                                  ip0 + 1u - z1::window_low_index(ip0, p.windowLog), first && last);
             const uint32_t nbSeq = uni(so.nbSeq), lastLL = uni(so.lastLL);
             P.mark(1);
             P.count(0, uni(so.rounds));

@@ -17,3 +17,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
 cat $out
 f=$(find gpurun_out/prof_defer_$TAG -name "*kernel_stats.csv" | head -1)
 cut -d, -f1-8 "$f" | head -20
+# per-phase wave-cycles of the deferred decode (the _prof library)
+PGN_DEFER_MIN_CHUNKS=1 timeout -k 10 200 python -u tools/phase_profile.py 20000 > gpurun_out/phase_defer_$TAG.log 2>&1 || exit 1
+tail -40 gpurun_out/phase_defer_$TAG.log
