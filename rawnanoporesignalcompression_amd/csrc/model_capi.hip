@@ -44,33 +44,44 @@ size_t z1m_sequences(const uint8_t* src, size_t n, uint32_t* out3, size_t maxSeq
 
 // The encoder's no-match certificate (pgn_zenc.h no_match_certificate), serially: 1 when the
 // level-1 search of the single-block frame src[0, n) provably finds no match.
+static uint32_t cert_fmix32(uint32_t x)
+{
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
+}
 int z1m_no_match_certificate(const uint8_t* src, size_t n)
 {
     if (n < 7 || n > kMaxSrc) return 0;
     const Params p = level1_params(n);
     const long ilimit = (long)n - 8;
-    const uint32_t slots = 8192 / 4;
-    uint32_t* set = (uint32_t*)calloc(slots, 4);
+    const uint32_t words = 8192 / 8, maxKeys = 2048;  // pgn_zenc.h kCertWords, kCertKeys
+    uint64_t* filt = (uint64_t*)calloc(words, 8);
     int ok = 1;
     uint32_t e = 257, k = 0;
     for (;; k++) {
-        if (k % 64 == 0 && 2 * (k + 64) > slots * 7 / 8) { ok = 0; break; }
+        if (k % 64 == 0 && 2 * (k + 64) > maxKeys) { ok = 0; break; }
         const long pk = (long)e - 256;
         e += e >> 7;
         if (!(pk + 1 < ilimit)) break;
         const uint64_t v8 = rd64(src + pk);
         if (rd32(src + pk + 1) == (uint32_t)(v8 >> 16)) { ok = 0; break; }  // repcode (offset 1) at ip0 + 2
-        const uint32_t keys[2] = {((uint32_t)v8 ^ (hash_word(v8, p.hashLog, p.mls) * 0x9E3779B1u)) | 1u,
-                                  ((uint32_t)(v8 >> 8) ^ (hash_word(v8 >> 8, p.hashLog, p.mls) * 0x9E3779B1u)) | 1u};
-        for (int j = 0; j < 2 && ok; j++) {
-            uint32_t s = (uint32_t)(((uint64_t)keys[j] * slots) >> 32);
-            while (set[s] && set[s] != keys[j]) s = s + 1 == slots ? 0 : s + 1;
-            if (set[s] == keys[j]) ok = 0;
-            set[s] = keys[j];
+        const uint32_t keys[2] = {(uint32_t)v8 ^ (hash_word(v8, p.hashLog, p.mls) * 0x9E3779B1u),
+                                  (uint32_t)(v8 >> 8) ^ (hash_word(v8 >> 8, p.hashLog, p.mls) * 0x9E3779B1u)};
+        for (int j = 0; j < 2 && ok; j++) {  // blocked Bloom filter: six bits of one 64-bit word
+            const uint32_t a = cert_fmix32(keys[j]), b = cert_fmix32(keys[j] ^ 0x5BD1E995u);
+            const uint64_t m = (1ull << (a & 63u)) | (1ull << ((a >> 6) & 63u)) | (1ull << ((a >> 12) & 63u)) |
+                               (1ull << ((a >> 18) & 63u)) | (1ull << ((a >> 24) & 63u)) | (1ull << (b & 63u));
+            uint64_t* w = filt + ((b >> 6) & (words - 1));
+            if ((*w & m) == m) ok = 0;
+            *w |= m;
         }
         if (!ok) break;
     }
-    free(set);
+    free(filt);
     return ok;
 }
 

@@ -17,14 +17,15 @@
 // one entry per 2^(tl-K) above it, the entry of a peek p (the stream's next tl bits) is
 //     idx = min(p, (p >> (tl - K)) + Cc),   Cc = T - (T >> (tl - K))
 // (both arguments are monotone in p and cross at T).  K is chosen per table for the smallest size;
-// a table that does not fit 512 entries (never seen on zstd level-1 output: 400-480 on the bench's
-// keys / M frames) is decoded in place by the frame decoder as before.
+// a table of more than 504 entries (never seen on zstd level-1 output: 400-480 on the bench's keys /
+// M frames) is decoded in place by the frame decoder as before.
 #pragma once
 // included by pgn_zdec.h (after the Huffman table builder; sDec, kHufLdsLog)
 
 namespace pgn {
 
-constexpr uint32_t kJobTab = 512;  // compact table entries (16-bit: nbBits | symbol << 8)
+constexpr uint32_t kJobTab = 512;     // compact table slots of a job (16-bit: nbBits | symbol << 8)
+constexpr uint32_t kJobTabUse = 504;  // entries a table may have: dec_huf_kernel keeps 504 per frame in LDS
 
 struct HufJob {
     uint64_t hp;      // the section's jump table; stream k starts at hp + 6 + len[0] + .. + len[k-1]
@@ -41,7 +42,7 @@ constexpr size_t kJobBytes = sizeof(HufJob) + 2 * kJobTab;
 // Frame decoder side (wave-uniform): the section at hp (4 streams, jump table jt01 / jt2, table in
 // sDec.tab with log tl) becomes job `job`.  Returns false -- and leaves the section to the caller's
 // in-place decoder, which then reports any corruption -- when the jump table is inconsistent or the
-// compact table exceeds kJobTab entries.
+// compact table exceeds kJobTabUse entries.
 __device__ __noinline__ bool huf_defer_section(uint8_t* job, unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst,
                                                uint32_t rs, uint32_t jt01, uint32_t jt2)
 {
@@ -82,7 +83,7 @@ __device__ __noinline__ bool huf_defer_section(uint8_t* job, unsigned tl, const 
             T = t;
         }
     }
-    if (size > kJobTab) return false;
+    if (size > kJobTabUse) return false;
     const uint32_t d = tl - K;
     const uint32_t Cc = T - (T >> d);
     uint16_t* tab = (uint16_t*)(job + sizeof(HufJob));

@@ -584,19 +584,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
 // ---------------------------------------------------------------------------------------------
 // Deferred four-stream Huffman sections (pgn_hufjob.h): one lane per stream, kHufFrames frames per
 // wave (lane 4f + k: stream k of frame f).  The wave takes the frames of one stream type (M, keys,
-// ...) of kHufFrames consecutive chunks, so its lanes' streams have the same length.  The compact
-// tables go to LDS; a lane reads its stream backwards through a 16-dword LDS ring ([slot][lane],
-// conflict-free) that it refills 16 bytes at a time from global memory one group ahead, and keeps a
-// 64-bit left-aligned bit container: a symbol is a peek of the top bits, the compact-table read, a
-// 64-bit shift by the code length (the entry's low byte) and the symbol byte packed four to a word;
-// every second symbol the container takes the next dword when it holds 32 bits or fewer (a code is
-// at most 11 bits, so two symbols always fit).  Words leave as aligned dword stores (the lane's
-// destination has any alignment: each store joins two words with v_alignbyte; the head and tail
-// bytes are byte stores).  After its symbols a stream must end exactly at its first bit (the strict
-// rule of huf_decode4_wave), else the frame's result is kDecErrHufStream.
+// ...) of kHufFrames consecutive chunks, so its lanes' streams have nearly the same length.  The
+// compact tables go to LDS; a lane keeps a 64-bit left-aligned bit container: a symbol is a peek of
+// the top bits, the compact-table read, a 64-bit shift by the code length (the entry's low byte) and
+// the symbol byte packed four to a word; every second symbol the container takes the next dword when
+// it holds 32 bits or fewer (a code is at most 11 bits, so two symbols always fit).
+//
+// Memory pattern (what the loop is built around; measured: tools/gpu_k2diag.sh).
+// * On gfx9 one counter (vmcnt) covers loads and stores and retires in order, so waiting for a load
+//   also waits for every store issued before it.  The loop issues the same memory operations every
+//   iteration, unconditionally (nothing is branched around): two 16-byte loads per 16-symbol
+//   iteration, consumed at the start of the next one.
+// * Input: the stream is read backwards in 16-byte blocks (block b at gtop - 16 b); dword j of block
+//   b sits at ring position 4 b + 3 - j of the lane's 16-dword LDS ring ([slot][lane],
+//   conflict-free), so block b is ring group b & 3.  An iteration consumes at most 176 bits (six
+//   dwords), so loading blocks bc + 2 and bc + 3 (bc: the block of the next dword) one iteration
+//   ahead always covers the next iteration and overwrites only consumed groups.
+// * Output: whole 128-byte lines.  A lane's 16-byte output blocks (each joins the previous and the
+//   current iteration's words with v_alignbyte, for any destination alignment) written one per
+//   iteration left 64 partial lines per wave open in L2; evicted half-written, they cost more than
+//   the decode (2.84 -> 1.63 ms per 20,000 chunks with the stores sent to one line).  So every lane
+//   starts 7 - m0 iterations late, m0 being its blocks before its first 128-byte boundary, and after
+//   an 8-iteration prologue (those blocks stored one by one) all lanes' lines end on the same
+//   iterations: the main loop runs trips of 8 iterations and stores each lane's line as 8
+//   consecutive 16-byte stores at the trip's end.
+// * Lanes outside their stream's iterations are frozen: their peek reads a 16-entry zero table (code
+//   length 0), their stores go to a junk line, their loads stay inside their stream.
+// The head and tail bytes are byte stores.  After its symbols a stream must end exactly at its first
+// bit (the strict rule of huf_decode4_wave), else the frame's result is kDecErrHufStream.
 // ---------------------------------------------------------------------------------------------
 constexpr int kHufFrames = 16;
-constexpr uint32_t kRing = 16;  // dwords per lane
+constexpr uint32_t kRing = 16;                  // dwords per lane (4 blocks)
+constexpr uint32_t kTabStride = kJobTabUse;     // LDS table entries per frame
+constexpr uint32_t kZeroTab = 16;               // frozen lanes' table entries
+constexpr size_t kHufJunkBytes = 64 * 128;      // frozen lanes' store target: a line per lane, shared by all waves
+static_assert((2 * kTabStride) % 16 == 0, "frame tables stay 16-byte aligned");
 
 __device__ __forceinline__ uint64_t shl64(uint64_t c, uint32_t e)  // c << (e & 63), one v_lshlrev_b64
 {
@@ -621,7 +643,7 @@ __device__ __forceinline__ uint32_t sel4(const uint4& v, uint32_t i)
 
 __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
 {
-    __shared__ __attribute__((aligned(16))) uint16_t tabs[kHufFrames * kJobTab];
+    __shared__ __attribute__((aligned(16))) uint16_t tabs[kHufFrames * kTabStride + kZeroTab];
     __shared__ uint32_t ring[kRing * 64];
     const uint32_t lane = (uint32_t)lane_id();
     const size_t G = a.G;
@@ -637,17 +659,22 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     const uint32_t flag = inb ? gld<uint32_t>(&J->flag) : 0u;
     const uint64_t fm = ballot(flag != 0);
     if (fm == 0) return;
-    // the pending frames' compact tables (1 KiB each, 16 bytes per lane; all loads in flight at once)
+    // the pending frames' compact tables (kTabStride entries each, 16 bytes per lane; all loads in
+    // flight at once)
     {
+        const uint32_t lt = lane < 63 ? lane : 62;
         uint4 tv[kHufFrames];
 #pragma unroll
         for (int ff = 0; ff < kHufFrames; ff++) {
             const size_t gf = (fm >> (4 * ff)) & 1u ? g0 + (size_t)ff : g0;
-            tv[ff] = gld<uint4>(a.jobs + (gf * kStreams + (size_t)s) * kJobBytes + sizeof(HufJob) + 16 * lane);
+            tv[ff] = gld<uint4>(a.jobs + (gf * kStreams + (size_t)s) * kJobBytes + sizeof(HufJob) + 16 * lt);
         }
 #pragma unroll
-        for (int ff = 0; ff < kHufFrames; ff++) *(uint4*)&tabs[ff * kJobTab + 8 * lane] = tv[ff];
+        for (int ff = 0; ff < kHufFrames; ff++)
+            if (lane < 63) *(uint4*)&tabs[ff * kTabStride + 8 * lane] = tv[ff];
+        if (lane < kZeroTab / 2) ((uint32_t*)&tabs[kHufFrames * kTabStride])[lane] = 0u;
     }
+    uint8_t* const junk = a.jobs + G * kStreams * kJobBytes + 128 * lane;
     // this lane's stream
     uint64_t hp = 0, dstp = 0;
     uint4 len = make_uint4(0, 0, 0, 0), prm = make_uint4(0, 11, 11, 0);
@@ -666,135 +693,201 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     uint8_t* sdst = (uint8_t*)dstp + (size_t)seg * q;
     const uint32_t lastB = (flag && sl) ? (uint32_t)gb(src + sl - 1) : 0u;
     bool bad = flag && lastB == 0;
-    if (bad) nsym = 0;
+    const bool live = flag && !bad;
+    if (!live) nsym = 0;
     const uint32_t sh1 = 32 - tl, sh2 = 32 - K;
-    const uint32_t tbase = f * kJobTab;
-    uint32_t* rl = ring + lane;  // slot t of this lane: rl[64 t]
-    // ---- bit reader: the top dword (holding the end marker) into the container, the rest of its
-    // 16-byte block and the next three blocks into the ring, two more blocks in registers (staged a
-    // super-group later, so their loads have 16 symbols' time to arrive)
-    const uint64_t e = (uint64_t)src + (sl ? sl - 1 : 0);
-    const uint64_t amin = (uint64_t)src & ~(uint64_t)15;  // reads stay in blocks holding stream bytes
-    uint64_t gaddr = e & ~(uint64_t)15;
+    // ---- bit reader.  Lanes without a stream read their junk line (readable, never decoded).
+    const uint64_t e = live ? (uint64_t)src + sl - 1 : (uint64_t)junk;
+    const uint64_t amin = live ? ((uint64_t)src & ~(uint64_t)15) : (uint64_t)junk;  // blocks holding stream bytes
+    const uint64_t gtop = e & ~(uint64_t)15;
+    const uint32_t bmax = (uint32_t)((gtop - amin) >> 4);
+#if PGN_K2_DIAG == 2  // diagnostic (wrong output): every block load reads the stream's top block
+    auto blk = [&](uint32_t b) { return gld<uint4>((const void*)(gtop - 16ull * (b < bmax ? b : bmax) * 0)); };
+#else
+    auto blk = [&](uint32_t b) { return gld<uint4>((const void*)(gtop - 16ull * (b < bmax ? b : bmax))); };
+#endif
+    auto stage = [&](uint32_t b, const uint4& v) {  // block b -> ring group b & 3 (highest address first)
+        uint32_t* r = ring + lane + 256u * (b & 3u);
+        r[0] = v.w;
+        r[64] = v.z;
+        r[128] = v.y;
+        r[192] = v.x;
+    };
     const uint32_t hb = lastB ? z1::highbit32(lastB) : 0u;
     const uint32_t i0 = (uint32_t)(e >> 2) & 3u;
-    const uint32_t v0 = (uint32_t)(e & 3u) * 8u + hb;  // valid bits of the top dword
+    const uint32_t v0 = live ? (uint32_t)(e & 3u) * 8u + hb : 0u;  // valid bits of the top dword
     const uint32_t totalBits = sl ? (sl - 1) * 8u + hb : 0u;
-    uint64_t C = 0;
-    uint32_t avail = 0, ins = 0, wpos = 0, nd = 0;
-    uint4 Ga = make_uint4(0, 0, 0, 0), Gb = Ga;
-    auto stage = [&](const uint4& blk) {  // a block's dwords, highest address first
-        rl[64 * (wpos & (kRing - 1))] = blk.w;
-        rl[64 * ((wpos + 1) & (kRing - 1))] = blk.z;
-        rl[64 * ((wpos + 2) & (kRing - 1))] = blk.y;
-        rl[64 * ((wpos + 3) & (kRing - 1))] = blk.x;
-        wpos += 4;
-    };
-    auto next_block = [&]() { gaddr = gaddr - 16 >= amin ? gaddr - 16 : amin; return gld<uint4>((const void*)gaddr); };
-    if (nsym || (flag && !bad)) {
-        const uint4 b0 = gld<uint4>((const void*)gaddr);
-        const uint4 b1 = next_block();
-        const uint4 b2 = next_block();
-        const uint4 b3 = next_block();
-        Ga = next_block();
-        Gb = next_block();
+    const uint32_t ins0 = 4 - i0;  // ring position of the dword below the top one
+    uint32_t ins = ins0, avail = v0;
+    uint64_t C;
+    uint32_t nd;
+    uint4 La, Lb;
+    uint32_t lb;  // block of La (Lb: lb + 1)
+    {
+        const uint4 b0 = blk(0), b1 = blk(1), b2 = blk(2);
+        lb = (ins >> 2) + 2;
+        La = blk(lb);
+        Lb = blk(lb + 1);
+        gst<uint4>(junk, make_uint4(0, 0, 0, 0));  // the prologue loop's pattern: loads, then one store
+        stage(0, b0);
+        stage(1, b1);
+        stage(2, b2);
         const uint32_t dw0 = sel4(b0, i0);
         C = v0 ? ((uint64_t)dw0 << (64 - v0)) : 0ull;
-        avail = v0;
-        if (i0 >= 1) rl[0] = sel4(b0, i0 - 1);
-        if (i0 >= 2) rl[64] = sel4(b0, i0 - 2);
-        if (i0 >= 3) rl[128] = sel4(b0, 0);
-        wpos = i0;
-        stage(b1);
-        stage(b2);
-        stage(b3);
-        // first refill (avail <= 31)
-        nd = rl[0];
-        C |= (uint64_t)nd << (32 - avail);
+        // first refill (avail <= 31), and a second one when the container still holds only 32
+        // bits: every pair of symbols starts with at least 33
+        nd = ring[64 * (ins & (kRing - 1)) + lane];
+        C |= shl64((uint64_t)nd, 32u - avail);
         avail += 32;
-        ins = 1;
-        nd = rl[64];
+        ins++;
+        nd = ring[64 * (ins & (kRing - 1)) + lane];
+        if (avail <= 32) {
+            C |= (uint64_t)nd;
+            avail += 32;
+            ins++;
+            nd = ring[64 * (ins & (kRing - 1)) + lane];
+        }
     }
+    // refill check: the dword goes into Cadd, which the next symbol ORs into the container only
+    // after its table read has been issued (its peek is valid without it: a pair of symbols starts
+    // with at least 33 bits and takes at most 22), so the refill is off the symbols' latency chain
+    uint64_t Cadd = 0;
     auto refill = [&]() {
         const bool m = avail <= 32;
         const uint32_t x = m ? nd : 0u;
-        C |= shl64((uint64_t)x, 32u - avail);
+        Cadd = shl64((uint64_t)x, 32u - avail);
         avail += m ? 32u : 0u;
         ins += m ? 1u : 0u;
-        nd = rl[64 * (ins & (kRing - 1))];
+        nd = ring[64 * (ins & (kRing - 1)) + lane];
     };
-    auto symbol = [&]() -> uint32_t {
+    // table byte addresses: entry min(p, pq) of the lane's table, p = peek >> (32 - tl),
+    // pq = (peek >> (32 - K)) + Cc; tb / tc carry the table base (the zero table when frozen)
+    const uint32_t tbLive = f * kTabStride, tbZero = kHufFrames * kTabStride;
+    uint32_t tb = tbLive, tc = Cc + tbLive, s1 = sh1;
+    auto symbol = [&](bool merge) -> uint32_t {
         const uint32_t hi = (uint32_t)(C >> 32);
-        const uint32_t p = hi >> sh1, pq = (hi >> sh2) + Cc;
-        const uint32_t ent = tabs[tbase + (p < pq ? p : pq)];
-        C = shl64(C, ent);
+        const uint32_t a1 = ((hi >> s1) + tb) << 1, a2 = ((hi >> sh2) + tc) << 1;
+#if PGN_K2_DIAG == 3  // diagnostic (wrong output): the table read replaced by arithmetic on the peek
+        const uint32_t ent = ((a1 < a2 ? a1 : a2) & 0xFF00u) | (4u + (hi >> 30));
+#else
+        const uint32_t ent = *(const uint16_t*)((const uint8_t*)tabs + (a1 < a2 ? a1 : a2));
+#endif
+        C = shl64(merge ? (C | Cadd) : C, ent);
         avail -= ent & 0xFFu;
         return ent;
     };
     auto word4 = [&]() -> uint32_t {  // four symbols (refill checks after the second and fourth)
-        const uint32_t e0 = symbol();
-        const uint32_t e1 = symbol();
+        const uint32_t e0 = symbol(true);
+        const uint32_t e1 = symbol(false);
         refill();
-        const uint32_t e2 = symbol();
-        const uint32_t e3 = symbol();
+        const uint32_t e2 = symbol(true);
+        const uint32_t e3 = symbol(false);
         refill();
         // byte 1 of each entry: the symbol
         return __builtin_amdgcn_perm(e1, e0, 0x0C0C0501u) | __builtin_amdgcn_perm(e3, e2, 0x05010C0Cu);
     };
-    // ---- output: super-groups of 16 symbols; aligned 16-byte stores D_j = output bytes
-    // [h + 16 (j - 1), h + 16 j), taken from the previous and the current super-group's words at the
-    // lane's byte offset h (a funnel: dword offset h / 4 by selects, byte offset h % 4 by v_alignbyte)
-    const uint32_t h = (16u - ((uint32_t)(uintptr_t)sdst & 15u)) & 15u;  // head bytes before the first aligned block
+    auto freeze = [&](bool fz) {  // frozen: code length 0 from the zero table (peek < 16)
+        tb = fz ? tbZero : tbLive;
+        tc = fz ? tbZero : Cc + tbLive;
+        s1 = fz ? 28u : sh1;
+    };
+    // ---- output geometry: block D_m = output bytes [h + 16 m, h + 16 m + 16) at A0 + 16 m (16-byte
+    // aligned), made in the iteration after super-group m from its words (P) and the next one's (W)
+    // at byte offset h (a funnel: dword offset h / 4 by selects, byte offset h % 4 by v_alignbyte).
+    // m0 blocks precede the lane's first 128-byte boundary; the lane's super-group li runs in global
+    // iteration li + 7 - m0, so D_{m0 + 8 t + k} comes out of global iteration 8 + 8 t + k.
+    const uint32_t h = (16u - ((uint32_t)(uintptr_t)sdst & 15u)) & 15u;  // head bytes before the first block
     uint8_t* A0 = sdst + h;
     const uint32_t rb = h & 3u;
     const bool q1 = (h >> 2) & 1u, q2 = (h >> 3) & 1u;
+    const uint32_t m0 = ((128u - ((uint32_t)(uintptr_t)A0 & 127u)) & 127u) >> 4;
+    const int sft = 7 - (int)m0;
+    const int sg = (int)(nsym / 16);  // super-groups of 16 symbols
+    const int nD = sg - 1;            // whole blocks D_0 .. D_{sg-2}
     uint32_t P[4] = {0, 0, 0, 0}, F[4] = {0, 0, 0, 0};
-    const uint32_t sgroups = nsym / 16;
-    const uint32_t maxGroups = wave_max(sgroups);
-    for (uint32_t it = 0; it < maxGroups; it++) {
-        if (it < sgroups) {
-            uint32_t W[4];
+    auto active = [&](int gi) { const int li = gi - sft; return li >= 0 && li < sg; };
+    // one global iteration: stage the blocks loaded an iteration ago, load the next two, decode 16
+    // symbols; returns block D_{li - 1}
+    auto iteration = [&](int gi) -> uint4 {
+        stage(lb, La);
+        stage(lb + 1, Lb);
+        lb = (ins >> 2) + 2;
+        La = blk(lb);
+        Lb = blk(lb + 1);
+        uint32_t W[4];
 #pragma unroll
-            for (int k = 0; k < 4; k++) W[k] = word4();
-            if (wpos - ins <= kRing - 8) {  // room for two blocks: the ones loaded a super-group ago
-                stage(Ga);
-                stage(Gb);
-                Ga = next_block();
-                Gb = next_block();
-            }
-            if (it == 0) {
+        for (int k = 0; k < 4; k++) W[k] = word4();
+        // X_m = word h / 4 + m of {P, W}: two levels of per-lane selects (no indexed array, which
+        // the compiler would place in scratch)
+        const uint32_t X0 = pick4(q1, q2, P[0], P[1], P[2], P[3]), X1 = pick4(q1, q2, P[1], P[2], P[3], W[0]),
+                       X2 = pick4(q1, q2, P[2], P[3], W[0], W[1]), X3 = pick4(q1, q2, P[3], W[0], W[1], W[2]),
+                       X4 = pick4(q1, q2, W[0], W[1], W[2], W[3]);
+        const uint4 D = make_uint4(__builtin_amdgcn_alignbyte(X1, X0, rb), __builtin_amdgcn_alignbyte(X2, X1, rb),
+                                   __builtin_amdgcn_alignbyte(X3, X2, rb), __builtin_amdgcn_alignbyte(X4, X3, rb));
+        const bool act = active(gi);
+        if (gi < 8) {  // the first super-group (li = 0) falls in the prologue: its head bytes
+            const bool first = gi == sft;
 #pragma unroll
-                for (int k = 0; k < 4; k++) F[k] = W[k];
-            } else {
-                // X_m = word h / 4 + m of {P, W}: two levels of per-lane selects (no indexed array,
-                // which the compiler would place in scratch)
-                const uint32_t X0 = pick4(q1, q2, P[0], P[1], P[2], P[3]), X1 = pick4(q1, q2, P[1], P[2], P[3], W[0]),
-                               X2 = pick4(q1, q2, P[2], P[3], W[0], W[1]), X3 = pick4(q1, q2, P[3], W[0], W[1], W[2]),
-                               X4 = pick4(q1, q2, W[0], W[1], W[2], W[3]);
-                gst<uint4>(A0 + 16 * (it - 1), make_uint4(__builtin_amdgcn_alignbyte(X1, X0, rb),
-                                                          __builtin_amdgcn_alignbyte(X2, X1, rb),
-                                                          __builtin_amdgcn_alignbyte(X3, X2, rb),
-                                                          __builtin_amdgcn_alignbyte(X4, X3, rb)));
-            }
+            for (int k = 0; k < 4; k++) F[k] = cnd(first, W[k], F[k]);
+        }
 #pragma unroll
-            for (int k = 0; k < 4; k++) P[k] = W[k];
+        for (int k = 0; k < 4; k++) P[k] = cnd(act, W[k], P[k]);
+        freeze(!active(gi + 1));
+        return D;
+    };
+    freeze(!active(0));
+    // prologue: global iterations 0 .. 7, the blocks before each lane's first line one by one
+    for (int gi = 0; gi < 8; gi++) {
+        const uint4 D = iteration(gi);
+        const int m = gi - sft - 1;
+#if PGN_K2_DIAG == 1  // diagnostic (wrong output): every store to the junk line
+        uint8_t* ad = junk;
+#else
+        uint8_t* ad = (m >= 0 && m < nD) ? A0 + 16 * m : junk;
+#endif
+        gst<uint4>(ad, D);
+    }
+    // the trip loop's pattern: loads, then eight stores (so its first wait is on the loads only)
+#pragma unroll
+    for (int k = 1; k < 8; k++) gst<uint4>(junk + 16 * k, make_uint4(0, 0, 0, 0));
+    // trips of 8 iterations: one whole line per lane
+    const int lines = nD > (int)m0 ? (nD - (int)m0 + 7) / 8 : 0;
+    const int trips = (int)wave_max((uint32_t)lines);
+    for (int t = 0; t < trips; t++) {
+        uint4 Dk[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) Dk[k] = iteration(8 + 8 * t + k);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int m = (int)m0 + 8 * t + k;
+#if PGN_K2_DIAG == 1
+            uint8_t* ad = junk + 16 * k;
+#else
+            uint8_t* ad = m < nD ? A0 + 16 * m : junk + 16 * k;
+#endif
+            gst<uint4>(ad, Dk[k]);
         }
     }
+    stage(lb, La);
+    stage(lb + 1, Lb);
+    freeze(false);
+    C |= Cadd;
+    Cadd = 0;
     // the head bytes (in the first super-group) and the pending bytes of the last one
-    if (sgroups) {
+    if (sg > 0) {
         for (uint32_t b = 0; b < h; b++) gst<uint8_t>(sdst + b, (uint8_t)(sel4(make_uint4(F[0], F[1], F[2], F[3]), b >> 2) >> (8 * (b & 3))));
-        const uint32_t J16 = 16 * sgroups - 16;  // first symbol of the last super-group
+        const uint32_t J16 = 16 * (uint32_t)sg - 16;  // first symbol of the last super-group
         for (uint32_t b = h; b < 16; b++)
             gst<uint8_t>(sdst + J16 + b, (uint8_t)(sel4(make_uint4(P[0], P[1], P[2], P[3]), b >> 2) >> (8 * (b & 3))));
     }
-    // the remaining symbols one by one
-    for (uint32_t i = 16 * sgroups; i < nsym; i++) {
-        const uint32_t ent = symbol();
+    // the remaining symbols one by one (fewer than 16: the ring holds them)
+    for (uint32_t i = 16 * (uint32_t)sg; i < nsym; i++) {
+        const uint32_t ent = symbol(true);
         refill();
         gst<uint8_t>(sdst + i, (uint8_t)(ent >> 8));
     }
     // exact end: the stream's bits consumed to its first bit
-    if (flag && !bad) bad = (v0 + 32u * ins - avail) != totalBits;
+    if (live) bad = (v0 + 32u * (ins - ins0) - avail) != totalBits;
     const uint64_t bm = ballot(bad);
     if (q == 0 && flag && ((bm >> (4 * f)) & 0xFull)) gst<int32_t>(&a.units[g * kStreams + (size_t)s].dres, (int32_t)z1::kDecErrHufStream);
 }
@@ -2119,7 +2212,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     c->lastDeferred = defer;
     const size_t nbuf = passes > 1 ? 2 : 1;
     const size_t unitBytes = align_up(G * kStreams * sizeof(DecUnit), 256);
-    const size_t bufBytes = G * stride + unitBytes + (defer ? G * kStreams * kJobBytes : 0);
+    const size_t bufBytes = G * stride + unitBytes + (defer ? G * kStreams * kJobBytes + kHufJunkBytes : 0);
     int rc = ensure_dec(c, slots, nbuf * bufBytes);
     if (rc) return rc;
     HIPCHK(hipEventRecord(c->ev[2], s));

@@ -240,19 +240,37 @@ __constant__ VisitChains kVisitChains = make_visit_chains();
 // with that hash.  So if no iteration's repcode holds and no two visited positions share their hash
 // and their first 4 bytes, the search finds nothing: the block is all literals (nbSeq 0, repeat
 // offsets unchanged), whatever the table holds -- and the table (a frame starts with an empty one,
-// tagged per frame) need not be read or written at all.  The pairs are found with a hash set of the
-// 32-bit keys hash ^ bytes in the codec LDS (the search's own LDS is not yet live); any repcode hit or
-// duplicate key -- a real candidate or a key collision -- returns false and the exact search runs.
-// For noise streams (the C5 S / M / Llow streams) this replaces the search's table round trips, the
-// bulk of the encoder's HBM bytes.
-constexpr uint32_t kCertSlots = kCodecLdsBytes / 4;
-// LDS compare-and-swap of an empty (0) word; returns the word's old value
-__device__ __forceinline__ uint32_t lds_cas(lds_u32* p, uint32_t val)
+// tagged per frame) need not be read or written at all.  The pairs are found with a blocked Bloom
+// filter over the keys (hash, 4 bytes) in the codec LDS (the search's own LDS is not yet live): a key
+// sets six bits of one 64-bit word with one LDS atomic OR, and finds its bits already set when an
+// equal key came before it (the atomics on one word are ordered, also between the lanes of one
+// instruction); any repcode hit or key whose bits were all set -- an equal key or a false positive,
+// about 4 % of 100,000-sample M streams -- returns false and the exact search runs.  For noise streams
+// (the C5 S / M / Llow streams) this replaces the search's table round trips, the bulk of the
+// encoder's HBM bytes.
+constexpr uint32_t kCertWords = kCodecLdsBytes / 8;  // 64-bit filter words
+constexpr uint32_t kCertKeys = 2048;                 // at most this many keys (false positives stay rare)
+__device__ __forceinline__ uint32_t fmix32(uint32_t x)
 {
-    uint32_t e = 0;
-    __hip_atomic_compare_exchange_strong(p, &e, val, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return e;
+    x ^= x >> 16;
+    x *= 0x85EBCA6Bu;
+    x ^= x >> 13;
+    x *= 0xC2B2AE35u;
+    x ^= x >> 16;
+    return x;
 }
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+// one key into the filter; true if its six bits were all set before
+__device__ __forceinline__ bool cert_insert(lds_u64* words, uint32_t x)
+{
+    const uint32_t a = fmix32(x), b = fmix32(x ^ 0x5BD1E995u);
+    const uint64_t m = (1ull << (a & 63u)) | (1ull << ((a >> 6) & 63u)) | (1ull << ((a >> 12) & 63u)) |
+                       (1ull << ((a >> 18) & 63u)) | (1ull << ((a >> 24) & 63u)) | (1ull << (b & 63u));
+    const uint32_t w = (b >> 6) & (kCertWords - 1u);
+    const uint64_t old = __hip_atomic_fetch_or(words + w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (old & m) == m;
+}
+static_assert((kCertWords & (kCertWords - 1)) == 0, "filter words: a power of two");
 __device__ __noinline__ bool no_match_certificate(const uint8_t* __restrict__ src, uint32_t n, unsigned hlog, unsigned mls,
                                                   uint32_t off1)
 {
@@ -262,43 +280,25 @@ __device__ __noinline__ bool no_match_certificate(const uint8_t* __restrict__ sr
     hlog = uni(hlog);
     mls = uni(mls);
     off1 = uni(off1);
-    lds_u32* set = (lds_u32*)sCodecLds;
-    for (uint32_t i = lane; i < kCertSlots; i += 64) set[i] = 0;
+    lds_u64* words = (lds_u64*)sCodecLds;
+    for (uint32_t i = lane; i < kCertWords; i += 64) words[i] = 0;
     lds_sync();
     const int32_t ilimit = (int32_t)n - 8;
     const uint32_t* E = kVisitChains.e[1];  // the first block of a frame: ip0 = 1, anchor = 0
     for (uint32_t ci = 0;; ci += 64) {
-        if (2 * (ci + 64) > kCertSlots * 7 / 8) return false;  // the set would fill up: the exact search decides
+        if (2 * (ci + 64) > kCertKeys) return false;  // too many keys: the exact search decides
         const int32_t pk = (int32_t)E[ci + lane] - 256;
         const bool valid = pk + 1 < ilimit;
         bool bad = false;
-        uint32_t k0 = 0, k1 = 0;
         if (valid) {
             const uint64_t v8 = ld64u(src + pk);
             bad = off1 > 0 && ld32u(src + pk + 2 - (int32_t)off1) == (uint32_t)(v8 >> 16);
             const uint32_t h0 = z1::hash_word(v8, hlog, mls), h1 = z1::hash_word(v8 >> 8, hlog, mls);
-            k0 = ((uint32_t)v8 ^ (h0 * 0x9E3779B1u)) | 1u;  // 0 marks an empty slot
-            k1 = ((uint32_t)(v8 >> 8) ^ (h1 * 0x9E3779B1u)) | 1u;
+            // ip0's key before ip1's: a lane's two keys are ordered too
+            if (cert_insert(words, (uint32_t)v8 ^ (h0 * 0x9E3779B1u))) bad = true;
+            if (cert_insert(words, (uint32_t)(v8 >> 8) ^ (h1 * 0x9E3779B1u))) bad = true;
         }
         if (ballot(bad)) return false;
-        // insert both keys (linear probing, LDS compare-and-swap); an equal key already there: a pair
-        uint32_t s0 = (uint32_t)(((uint64_t)k0 * kCertSlots) >> 32), s1 = (uint32_t)(((uint64_t)k1 * kCertSlots) >> 32);
-        bool d0 = !valid, d1 = !valid, dup = false;
-        while (ballot(!d0 || !d1)) {
-            if (!d0) {
-                const uint32_t old = lds_cas(set + s0, k0);
-                if (old == 0u) d0 = true;
-                else if (old == k0) d0 = dup = true;
-                else s0 = s0 + 1 == kCertSlots ? 0u : s0 + 1;
-            }
-            if (!d1) {
-                const uint32_t old = lds_cas(set + s1, k1);
-                if (old == 0u) d1 = true;
-                else if (old == k1) d1 = dup = true;
-                else s1 = s1 + 1 == kCertSlots ? 0u : s1 + 1;
-            }
-        }
-        if (ballot(dup)) return false;
         if (ballot(!valid)) return true;  // the chain has left the block
     }
 }
@@ -350,6 +350,9 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
     uint32_t off1 = rep0, off2 = rep1, offSaved = 0;
     if (off2 > maxRep) { offSaved = off2; off2 = 0; }
     if (off1 > maxRep) { offSaved = off1; off1 = 0; }
+#ifdef PGN_NO_CERT  // A/B builds: the exact search only
+    single = false;
+#endif
     if (single && no_match_certificate(src, end, hlog, mls, off1)) {  // the whole frame is one literals block
         SearchOut r;
         r.nbSeq = 0;
