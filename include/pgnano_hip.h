@@ -31,7 +31,8 @@ typedef enum pgn_status {
     PGN_ERR_ZSTD_COMPRESS = 5,    /* "Failed to compress ..."                        C5.hpp:340-342 */
     PGN_ERR_CORRUPT = 6,          /* input on which the reference reads out of bounds (UB there) */
     PGN_ERR_UNSUPPORTED = 9,      /* chunk above PGN_MAX_CHUNK_SAMPLES; decode: frames claiming more than 5 bytes
-                                     per sample of the chunk (the intermediate's capacity) */
+                                     per sample of the call's largest chunk, rounded up to 4,096 samples (the
+                                     intermediate's capacity; calls of up to 64 chunks: 262,144 samples) */
     PGN_ERR_INVALID_ARG = 10,
     PGN_ERR_HIP = 11,             /* HIP runtime failure (message in pgn_last_error) */
     PGN_ERR_NO_DEVICE = 12,

@@ -614,7 +614,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
 // bit (the strict rule of huf_decode4_wave), else the frame's result is kDecErrHufStream.
 // ---------------------------------------------------------------------------------------------
 constexpr int kHufFrames = 16;
-constexpr uint32_t kRing = 16;                  // dwords per lane (4 blocks)
+#ifndef PGN_K2_PF
+#define PGN_K2_PF 1
+#endif
+constexpr uint32_t kPf = PGN_K2_PF;             // iterations between a block load and its staging
+constexpr uint32_t kRing = 16 * kPf;            // dwords per lane (4 kPf blocks)
+constexpr uint32_t kRingBlocks = kRing / 4;
 constexpr uint32_t kTabStride = kJobTabUse;     // LDS table entries per frame
 constexpr uint32_t kZeroTab = 16;               // frozen lanes' table entries
 constexpr size_t kHufJunkBytes = 64 * 128;      // frozen lanes' store target: a line per lane, shared by all waves
@@ -706,8 +711,8 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
 #else
     auto blk = [&](uint32_t b) { return gld<uint4>((const void*)(gtop - 16ull * (b < bmax ? b : bmax))); };
 #endif
-    auto stage = [&](uint32_t b, const uint4& v) {  // block b -> ring group b & 3 (highest address first)
-        uint32_t* r = ring + lane + 256u * (b & 3u);
+    auto stage = [&](uint32_t b, const uint4& v) {  // block b -> ring group b % kRingBlocks (highest address first)
+        uint32_t* r = ring + lane + 256u * (b & (kRingBlocks - 1u));
         r[0] = v.w;
         r[64] = v.z;
         r[128] = v.y;
@@ -721,17 +726,26 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     uint32_t ins = ins0, avail = v0;
     uint64_t C;
     uint32_t nd;
-    uint4 La, Lb;
-    uint32_t lb;  // block of La (Lb: lb + 1)
+    // blocks in flight: slot 0 was loaded kPf iterations ago (staged next), slot kPf - 1 last
+    uint4 La[kPf], Lb[kPf];
+    uint32_t lb[kPf];  // block of La (Lb: lb + 1)
+    auto issue = [&](uint32_t slot) {
+        lb[slot] = (ins >> 2) + 2 * kPf;
+        La[slot] = blk(lb[slot]);
+        Lb[slot] = blk(lb[slot] + 1);
+    };
     {
-        const uint4 b0 = blk(0), b1 = blk(1), b2 = blk(2);
-        lb = (ins >> 2) + 2;
-        La = blk(lb);
-        Lb = blk(lb + 1);
-        gst<uint4>(junk, make_uint4(0, 0, 0, 0));  // the prologue loop's pattern: loads, then one store
-        stage(0, b0);
-        stage(1, b1);
-        stage(2, b2);
+        uint4 b0v[2 * kPf + 2];
+#pragma unroll
+        for (uint32_t k = 0; k < 2 * kPf + 2; k++) b0v[k] = blk(k);
+#pragma unroll
+        for (uint32_t k = 0; k < kPf; k++) {  // the loop's pattern: two loads, then one store
+            issue(k);
+            gst<uint4>(junk, make_uint4(0, 0, 0, 0));
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 2 * kPf + 2; k++) stage(k, b0v[k]);
+        const uint4 b0 = b0v[0];
         const uint32_t dw0 = sel4(b0, i0);
         C = v0 ? ((uint64_t)dw0 << (64 - v0)) : 0ull;
         // first refill (avail <= 31), and a second one when the container still holds only 32
@@ -809,11 +823,15 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     // one global iteration: stage the blocks loaded an iteration ago, load the next two, decode 16
     // symbols; returns block D_{li - 1}
     auto iteration = [&](int gi) -> uint4 {
-        stage(lb, La);
-        stage(lb + 1, Lb);
-        lb = (ins >> 2) + 2;
-        La = blk(lb);
-        Lb = blk(lb + 1);
+        stage(lb[0], La[0]);
+        stage(lb[0] + 1, Lb[0]);
+#pragma unroll
+        for (uint32_t k = 0; k + 1 < kPf; k++) {
+            lb[k] = lb[k + 1];
+            La[k] = La[k + 1];
+            Lb[k] = Lb[k + 1];
+        }
+        issue(kPf - 1);
         uint32_t W[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) W[k] = word4();
@@ -837,6 +855,8 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     };
     freeze(!active(0));
     // prologue: global iterations 0 .. 7, the blocks before each lane's first line one by one
+    // (unrolled: the in-flight slots rotate by renaming, not by copies that would wait for the loads)
+#pragma unroll
     for (int gi = 0; gi < 8; gi++) {
         const uint4 D = iteration(gi);
         const int m = gi - sft - 1;
@@ -868,8 +888,11 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
             gst<uint4>(ad, Dk[k]);
         }
     }
-    stage(lb, La);
-    stage(lb + 1, Lb);
+#pragma unroll
+    for (uint32_t k = 0; k < kPf; k++) {
+        stage(lb[k], La[k]);
+        stage(lb[k] + 1, Lb[k]);
+    }
     freeze(false);
     C |= Cadd;
     Cadd = 0;
@@ -2220,7 +2243,11 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     if (rc) return rc;
     // the merge of pass p runs on the side stream beside pass p + 1's zstd kernel; a single pass
     // stays on the caller's stream
+#ifdef PGN_SERIAL_DECODE  // diagnostic builds: every decode kernel on the caller's stream (isolated kernel times)
+    const hipStream_t sideS = s;
+#else
     const hipStream_t sideS = passes > 1 ? c->side : s;
+#endif
     if (passes > 1) {
         HIPCHK(hipEventRecord(c->evFork, s));
         HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
@@ -2248,9 +2275,9 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         const int lrc = take_lookback(c, s, a.lookback, a.epoch);
         if (lrc) return lrc;
     }
-    // pass p: parse + zstd on the caller's stream into buffer p % 2, merge on the side stream.  The
-    // merge of pass p overlaps the zstd kernel of pass p+1; a buffer is parsed into again only after
-    // the merge of the pass before last has read it.
+    // pass p: parse + zstd on the caller's stream into buffer p % 2, the deferred Huffman sections and
+    // the merge on the side stream.  Those of pass p overlap the zstd kernel of pass p+1; a buffer is
+    // parsed into again only after the merge of the pass before last has read it.
     for (size_t p = 0; p < passes; p++) {
         const int b = (int)(p & 1);
         uint8_t* buf = c->decChunks + (size_t)b * bufBytes;
@@ -2268,12 +2295,21 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         if (coop)
             hipLaunchKernelGGL(dec_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopWaves), 0, s, a);
         else hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-        if (defer)  // the deferred sections: kHufFrames frames of one stream type per wave
+#ifdef PGN_K2_MAIN  // A/B builds: the deferred sections on the caller's stream, before the next pass's frames
+        if (defer)
             hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, s, a);
+#endif
         if (passes > 1) {
             HIPCHK(hipEventRecord(c->evStage[b], s));
             HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
         }
+#ifndef PGN_K2_MAIN
+        // the deferred sections (kHufFrames frames of one stream type per wave) on the side stream,
+        // ahead of the pass's merge: they overlap the next pass's frame decode (LDS- and
+        // latency-bound beside a scalar- and latency-bound kernel)
+        if (defer)
+            hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, sideS, a);
+#endif
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
         else if (a.lookback)  // few chunks: kMergeRanges single-wave workgroups per chunk
             hipLaunchKernelGGL(dec_merge_lb_kernel, dim3((unsigned)(G * kMergeRanges)), dim3(64), 0, sideS, a);
@@ -2493,6 +2529,10 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
         rc = finish_scan(c, count, maxN, &maxAll);
         capCall = call_cap(maxAll);
     }
+    // small calls (the per-chunk ones) keep the full capacity: a frame is then decoded up to its own
+    // content size, as the reference does, and the chunk ends with its statuses (e.g. "Remaining
+    // data" for samples fewer than the frames hold) rather than PGN_ERR_UNSUPPORTED
+    if (nchunks <= kCoopMaxChunks) capCall = kPassSamples;
     if (rc == PGN_OK)
         rc = launch_decode_impl(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                                 d_sample_counts, d_status, s, capCall);
