@@ -43,8 +43,8 @@ constexpr size_t kJobBytes = sizeof(HufJob) + 2 * kJobTab;
 // sDec.tab with log tl) becomes job `job`.  Returns false -- and leaves the section to the caller's
 // in-place decoder, which then reports any corruption -- when the jump table is inconsistent or the
 // compact table exceeds kJobTabUse entries.
-__device__ __noinline__ bool huf_defer_section(uint8_t* job, unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst,
-                                               uint32_t rs, uint32_t jt01, uint32_t jt2)
+__device__ __forceinline__ bool huf_defer_body(uint8_t* job, unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst,
+                                              uint32_t rs, uint32_t jt01, uint32_t jt2)
 {
     const uint32_t lane = (uint32_t)lane_id();
     job = uni(job);
@@ -100,6 +100,11 @@ __device__ __noinline__ bool huf_defer_section(uint8_t* job, unsigned tl, const 
         gst<uint32_t>(&J->flag, 1u);
     }
     return true;
+}
+__device__ __noinline__ bool huf_defer_section(uint8_t* job, unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst,
+                                               uint32_t rs, uint32_t jt01, uint32_t jt2)
+{
+    return huf_defer_body(job, tl, hp, remain, dst, rs, jt01, jt2);
 }
 
 }  // namespace pgn

@@ -559,11 +559,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
     PhaseProf P;
     P.init(a.prof);
     const size_t G = a.G, units = (size_t)a.nu * G;
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(a.queue, 1u);
     while (true) {
-        uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(a.queue, 1u);
-        u = __builtin_amdgcn_readfirstlane(u);
+        const uint32_t u = __builtin_amdgcn_readfirstlane(tk);
         if (u >= units) break;
+        if (lane == 0) tk = atomicAdd(a.queue, 1u);
         const int s = a.nu == 1 ? 0 : unit_stream((uint32_t)(u / G));
         const size_t g = u % G;
         const size_t c = a.base + g;
@@ -574,7 +575,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
         // destination capacity: the frame content size (C5.hpp:588-667 sizes each stream's slot
         // exactly); VBZ's intermediate carries svb16's 16 padding bytes (signal_compression.cpp:112-118)
         const size_t cap = a.nu == 1 ? (size_t)d.cs + kVbzPadding : (size_t)d.cs;
-        const long r = zstd_decompress_wave(a.in + d.src, d.len, a.inter + g * a.interStride + d.interOff, cap, S, P);
+        uint8_t* const dst = a.inter + g * a.interStride + d.interOff;
+        // (the record's fields are read again for the call: kept live across the fast path they
+        // pushed this kernel from 37 to 186 spilled VGPRs)
+        P.mark(3);
+        long r = dec_frame_fast(a.in + d.src, d.len, dst, cap, S.job, S.htab, P);
+        P.mark(2);  // (phase 2: the fast path, or its fall-through)
+        if (r < 0) r = zstd_decompress_wave(a.in + d.src, d.len, dst, cap, S, P);
         if (lane == 0) d.dres = (int32_t)r;
         wave_sync();
     }

@@ -328,17 +328,28 @@ __device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxS
 
 // Returns header bytes consumed (0 = corrupt); *tlOut = table log, *minNbOut = its shortest code.
 // Fills sDec.tab, or gt (4096 entries in HBM) for a 12-bit table.
-__device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
-                                                     unsigned* minNbOut)
+// hw: when not null, the frame's header window (loaded at frame offset 0) and src at frame offset hoff:
+// the description is staged from it (lane-permute reads, no memory round trip) when it lies inside
+__device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
+                                                       unsigned* minNbOut, const HdrWin* hw = nullptr, uint32_t hoff = 0,
+                                                       PhaseProf* Pp = nullptr)
 {
     const int lane = lane_id();
     src = uni(src);
     gt = uni(gt);
     srcSize = uni((uint64_t)srcSize);
     if (srcSize < 1) return 0;
-    // stage the description (at most 129 bytes are part of it)
+    // stage the description (at most 129 bytes are part of it; the bytes read are [0, 129))
     const uint32_t nst = srcSize < 256 ? (uint32_t)srcSize : 256u;
-    for (uint32_t i = (uint32_t)lane; i < 272; i += 64) sDec.hbuf[i] = i < nst ? gb(src + i) : (uint8_t)0;
+    if (hw && hw->base == 0 && hoff + 144 <= 256) {
+        for (uint32_t i = (uint32_t)lane; i < 272; i += 64) {
+            const uint32_t fo = hoff + i, sl = fo >> 2 < 63 ? fo >> 2 : 63u;
+            const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * sl), (int)hw->w);
+            sDec.hbuf[i] = (i < nst && i < 144) ? (uint8_t)(v >> (8 * (fo & 3))) : (uint8_t)0;
+        }
+    } else {
+        for (uint32_t i = (uint32_t)lane; i < 272; i += 64) sDec.hbuf[i] = i < nst ? gb(src + i) : (uint8_t)0;
+    }
     lds_sync();
     const uint32_t iSize = sDec.hbuf[0];
     uint32_t nbW = 0;
@@ -365,6 +376,7 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
         if (!wdtable_build(sDec.wnorm, maxSV, tl)) return 0;
         // FSE weight stream: backward bit container over the staged bytes, the decode table in a
         // VGPR (entry u in lane u: newState | symbol << 16 | nbBits << 24, read with v_readlane)
+        if (Pp) Pp->mark(12);
         const uint8_t* bs = sDec.hbuf + 1 + nc;
         const int32_t bl = (int32_t)(iSize - nc);
         const uint32_t last = bs[bl - 1];
@@ -411,6 +423,7 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
         }
         used = iSize + 1;
     }
+    if (Pp) Pp->mark(15);
     lds_sync();
     // HUF_readStats tail: implied last weight and table log (weights > 12 are corrupt)
     uint32_t w4[4];
@@ -508,6 +521,12 @@ __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t 
     *tlOut = tl;
     *minNbOut = tl + 1 - wmax;
     return used;
+}
+// the frame decoder's call (one copy of the code for its many call sites); dec_frame_fast inlines the body
+__device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
+                                                     unsigned* minNbOut)
+{
+    return huf_build_dtable_body(src, srcSize, tlOut, gt, minNbOut);
 }
 
 }  // namespace pgn
@@ -1119,6 +1138,73 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
     }
     wave_sync();
     return (long)op;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The batch decoder's fast path for the two frame shapes that make up most of a C5 chunk: a frame
+// that is one raw block (the S and Llow streams) and a frame that is one compressed block of
+// literals only with four Huffman streams and a new table (keys, M), whose streams are left to
+// dec_huf_kernel as a job.  Everything is inlined into the kernel's unit loop: zstd_decompress_wave
+// is a call, and at 96 VGPRs the call's spills, callee-saved registers and by-value arguments went
+// through the wave's private stack -- ~120 KB of HBM writes per chunk (profiles/r04_*traffic*).
+// Returns the decoded size, or -1 when the frame is anything else or anything is out of the
+// ordinary (sizes, end of input, a table the job cannot hold): the caller then runs
+// zstd_decompress_wave, which reaches the same result or reports the error, so statuses and bytes
+// are the general decoder's in every case.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, size_t srcSize, uint8_t* __restrict__ dst,
+                                               size_t dstCap, uint8_t* job, uint16_t* htab, PhaseProf& P)
+{
+    if (srcSize < 9) return -1;
+    HdrWin hw;
+    hw_load(hw, src, srcSize, 0);
+    if (hw_u32(hw, src, 0) != z1::kMagic) return -1;
+    const uint32_t fhd = hw_byte(hw, src, 4);
+    const unsigned checksum = (fhd >> 2) & 1, singleSegment = (fhd >> 5) & 1, fcsFlag = fhd >> 6;
+    if (fhd & 0x0B) return -1;  // reserved bit, or a dictionary id
+    size_t ip = 5 + (singleSegment ? 0 : 1);
+    const unsigned fcsSize = (fcsFlag == 0) ? (singleSegment ? 1 : 0) : (1u << fcsFlag);
+    if (fcsSize == 8 || ip + fcsSize + 3 > srcSize) return -1;
+    uint64_t fcs = 0;
+    if (fcsSize == 1) fcs = hw_byte(hw, src, ip);
+    else if (fcsSize == 2) fcs = (uint64_t)hw_u16(hw, src, ip) + 256;
+    else if (fcsSize == 4) fcs = hw_u32(hw, src, ip);
+    ip += fcsSize;
+    const uint32_t bh = hw_u24(hw, src, ip);
+    ip += 3;
+    const size_t bsize = bh >> 3;
+    const unsigned btype = (bh >> 1) & 3;
+    P.mark(7);
+    // one last block, and the frame (its checksum included) ends where the unit does
+    if (!(bh & 1) || bsize > srcSize - ip || ip + bsize + (checksum ? 4 : 0) != srcSize) return -1;
+    if (btype == z1::kBtRaw) {
+        if (bsize > dstCap || (fcsSize > 0 && bsize != fcs)) return -1;
+        wave_copy8(dst, src + ip, bsize);
+        P.mark(5);
+        return (long)bsize;
+    }
+    if (btype != z1::kBtCompressed || job == nullptr || bsize > z1::kMaxSrc || bsize < 5) return -1;
+    const uint32_t lhc = hw_u32(hw, src, ip);
+    const unsigned ltype = lhc & 3, sf = (lhc >> 2) & 3;
+    if (ltype != z1::kSetCompressed || sf == 0) return -1;
+    size_t lh, rs, cs;
+    if (sf == 1) { lh = 3; rs = (lhc >> 4) & 0x3FF; cs = (lhc >> 14) & 0x3FF; }
+    else if (sf == 2) { lh = 4; rs = (lhc >> 4) & 0x3FFF; cs = lhc >> 18; }
+    else { lh = 5; rs = (lhc >> 4) & 0x3FFFF; cs = (lhc >> 22) + ((size_t)hw_byte(hw, src, ip + 4) << 10); }
+    if (rs > z1::kMaxSrc || rs > dstCap || lh + cs + 1 != bsize || (fcsSize > 0 && rs != fcs)) return -1;
+    if (hw_byte(hw, src, ip + lh + cs) != 0) return -1;  // the sequences section: none
+    const uint8_t* hp = src + ip + lh;
+    unsigned tl = 0, mn = 1;
+    const size_t hsz = huf_build_dtable_body(hp, cs, &tl, htab, &mn, &hw, (uint32_t)(ip + lh), &P);  // (a 12-bit table goes to htab)
+    P.mark(1);
+    if (hsz == 0 || tl > kHufLdsLog || cs - hsz < 6) return -1;
+    hp += hsz;
+    const size_t remain = cs - hsz;
+    const size_t jp = (size_t)(hp - src);
+    const uint32_t jt01 = hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16);
+    const uint32_t jt2 = hw_u16(hw, src, jp + 4);
+    if (!huf_defer_body(job, tl, hp, remain, dst, (uint32_t)rs, jt01, jt2)) return -1;
+    return (long)rs;
 }
 
 }  // namespace pgn

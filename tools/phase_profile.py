@@ -12,9 +12,9 @@ from rawnanoporesignalcompression_amd import PGNanoCodec
 
 ENC = ["split", "search", "lit_gather", "hist", "sort", "hdr(writeCTable)", "huf_encode", "raw_lit", "seq",
        "frame_finish", "assemble", "tree_merge", "tree_depth", "tree_maxheight", "tree_canon"]
-DEC = ["parse/merge_wait", "huf_table", "huf_copy(ph3)", "unit_fetch", "seq_exec(rest)", "raw_copy", "merge",
-       "lit_hdr", "huf_store(passB)", "seq_tables", "seq_bits", "huf_spec(passA)", "huf_sync", "seq_decode",
-       "seq_copy", "seq_tail"]
+DEC = ["parse/merge_wait", "huf_table/tab_fill", "fast_path/huf_copy", "unit_fetch", "seq_exec(rest)", "raw_copy", "merge",
+       "lit_hdr", "huf_store(passB)", "seq_tables", "seq_bits", "huf_spec(passA)", "huf_sync/tab_stage", "seq_decode",
+       "seq_copy", "seq_tail/tab_weights"]
 R = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 S = 100000
 c = PGNanoCodec(0)
