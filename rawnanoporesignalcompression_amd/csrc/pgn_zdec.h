@@ -382,14 +382,16 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
         const uint32_t last = bs[bl - 1];
         if (last == 0) return 0;
         int32_t pos = (bl - 1) * 8 + (int32_t)z1::highbit32(last);
-        auto word = [&](int32_t wi) -> uint32_t {  // stream bytes [4wi, 4wi + 4), zero outside
-            uint32_t v = 0;
+        // the stream (<= 128 bytes) in one VGPR, lane l holding bytes [4l, 4l + 4) (zero past bl): a
+        // refill is one readlane, and the container, the position and the states stay scalar
+        uint32_t bsv = 0;
 #pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const int32_t i = 4 * wi + b;
-                v |= (i >= 0 && i < bl) ? ((uint32_t)bs[i] << (8 * b)) : 0u;
-            }
-            return v;
+        for (int b = 0; b < 4; b++) {
+            const int32_t i = 4 * lane + b;
+            bsv |= (i < bl) ? ((uint32_t)bs[i] << (8 * b)) : 0u;
+        }
+        auto word = [&](int32_t wi) -> uint32_t {  // stream bytes [4wi, 4wi + 4), zero outside
+            return (wi >= 0 && wi < 32) ? readlane_u32(bsv, wi) : 0u;
         };
         int32_t cl = ((pos >> 5) - 1) * 32;  // C holds bits [cl, cl + 64)
         uint64_t C = (uint64_t)word(cl >> 5) | ((uint64_t)word((cl >> 5) + 1) << 32);

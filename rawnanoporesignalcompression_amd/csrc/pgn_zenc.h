@@ -1195,10 +1195,11 @@ __device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t
                     const uint32_t vST = ((uint32_t)lane < (1u << tableLog)) ? (uint32_t)L.fct.stateTable[lane] : 0u;
                     const uint32_t vDN = ((uint32_t)lane <= maxW) ? L.fct.deltaNbBits[lane] : 0u;
                     const uint32_t vDF = ((uint32_t)lane <= maxW) ? (uint32_t)L.fct.deltaFindState[lane] : 0u;
+                    // weight of symbol i: byte i & 3 of lane i >> 2 of W4 (one readlane and a scalar bit-field
+                    // extract: selecting among w[0..3] by i >> 6 compiled to a chain of scalar branches per symbol)
+                    const uint32_t W4 = reinterpret_cast<const uint32_t*>(L.weights)[lane];
                     auto wsym = [&](uint32_t i) -> uint32_t {
-                        const uint32_t r = i >> 6;
-                        const uint32_t v = r == 0 ? w[0] : (r == 1 ? w[1] : (r == 2 ? w[2] : w[3]));
-                        return readlane_u32(v, (int)(i & 63u));
+                        return (readlane_u32(W4, (int)(i >> 2)) >> (8u * (i & 3u))) & 0xFFu;
                     };
                     uint32_t wv = 0, nw = 0, nacc = 0;
                     uint64_t acc = 0;
