@@ -113,6 +113,15 @@ template <bool C4> struct ClassOffsets {
     static constexpr uint32_t t1 = C4 ? 15u : 16u, t2 = C4 ? 255u : 272u;  // class >= 2 iff v > t1, 3 iff v > t2
 };
 
+// (m & a) | (~m & b) as one v_bfi_b32 (written as and/or or ?:, the selects become compare +
+// cndmask pairs)
+__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
+
 // One 1024-sample step (Full: every sample of the step exists).  Returns the lane's key word.
 // Full steps take the lane's 32 sample bytes already loaded (a, b: prefetched one step ahead).
 // Deltas, zig-zag and classes are computed two samples per instruction (packed 16-bit halves):
@@ -193,9 +202,9 @@ __device__ __forceinline__ uint32_t split_step(const uint4& a, const uint4& b, c
         // class 1: S window at its rank among the lane's class-1 samples; class 2: M likewise;
         // classes 0 and 3: the discard slot (empty mask, rank 0)
         const uint32_t below = (1u << (2 * m)) - 1u;
-        const bool isS = (m1 >> (2 * m)) & 1u, isM = (m2 >> (2 * m)) & 1u;
-        const uint32_t msk = isS ? m1 : (isM ? m2 : 0u);
-        const uint32_t base = isS ? baseS : (isM ? baseM : dS);
+        const uint32_t bS = (uint32_t)__builtin_amdgcn_sbfe((int)m1, 2 * m, 1), bM = (uint32_t)__builtin_amdgcn_sbfe((int)m2, 2 * m, 1);
+        const uint32_t msk = bfi32(bS, m1, m2 & bM);
+        const uint32_t base = bfi32(bS, baseS, bfi32(bM, baseM, dS));
         const uint32_t at = base + (uint32_t)__builtin_popcount(msk & below);
         wb[at] = (uint8_t)(val[m >> 1] >> (16 * (m & 1)));
     }
@@ -482,14 +491,6 @@ __device__ __forceinline__ void put_bytes16(uint16_t* d, const uint4& v, uint32_
     uint4* q = (uint4*)d;
     q[0] = make_uint4(o[0], o[1], o[2], o[3]);
     q[1] = make_uint4(o[4], o[5], o[6], o[7]);
-}
-
-// (m & a) | (~m & b) as one v_bfi_b32
-__device__ __forceinline__ uint32_t bfi32(uint32_t m, uint32_t a, uint32_t b)
-{
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-    return r;
 }
 
 // Merge step over 1024 samples: lane l decodes the 16 consecutive samples t + 16l .. t + 16l + 15,

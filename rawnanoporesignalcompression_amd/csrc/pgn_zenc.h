@@ -629,11 +629,13 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
     // the next step's 16-byte block is loaded one step ahead
     uint4 nv = make_uint4(0, 0, 0, 0);
     if ((int32_t)len - 16 - (int32_t)(16 * lane) >= 0) nv = gld<uint4>(src + (len - 16 - 16 * lane));
-    for (uint32_t r0 = 0; r0 < len; r0 += 1024) {
+    // a step of 1024 emissions; FULL (every lane's 16 emissions exist: all but the last step) reads
+    // the code table without per-symbol masks (predicated LDS reads cost an exec-mask round per symbol)
+    auto step = [&](auto FULL, uint32_t r0) {
         // my 16 emissions r0 + 16*lane + j are bytes len-1-r of src: one 16-byte block, reversed
         const int32_t a = (int32_t)len - 16 - (int32_t)(r0 + 16 * lane);
         uint32_t wv[4];
-        if (a >= 0) {
+        if (FULL || a >= 0) {
             const uint4 v = nv;
             wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
             if (a - 1024 >= 0) nv = gld<uint4>(src + (a - 1024));
@@ -661,7 +663,8 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
             for (int jj = 0; jj < 4; jj++) {
                 const int j = 4 * g + jj;
                 const uint32_t sym = (wv[(15 - j) >> 2] >> (8 * ((15 - j) & 3))) & 0xFFu;
-                const uint32_t cwj = (j < nvalid) ? cw[sym] : 0u;
+                uint32_t cwj = cw[sym];
+                if (!FULL) cwj = (j < nvalid) ? cwj : 0u;
                 acc |= (uint64_t)(cwj & 0xFFFFu) << n;
                 n += cwj >> 16;
             }
@@ -699,7 +702,10 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
         lds_sync();
         winLo += complete * 32;
         bitBase += stepBits;
-    }
+    };
+    uint32_t r0 = 0;
+    for (; r0 + 1024 <= len; r0 += 1024) step(std::true_type{}, r0);
+    if (r0 < len) step(std::false_type{}, r0);
     // end mark, then the last partial bytes
     if (lane == 0) {
         const uint32_t rel = totalBits - winLo;
