@@ -285,14 +285,28 @@ __device__ __noinline__ bool no_match_certificate(const uint8_t* __restrict__ sr
     lds_sync();
     const int32_t ilimit = (int32_t)n - 8;
     const uint32_t* E = kVisitChains.e[1];  // the first block of a frame: ip0 = 1, anchor = 0
+    // software pipeline: a round's bytes were loaded during the round before, and its positions
+    // two rounds ahead (the chain is data-independent), so a round waits on no memory round trip
+    auto loads = [&](int32_t p, uint64_t& v, uint32_t& r) {
+        if (p + 1 < ilimit) {
+            v = ld64u(src + p);
+            r = off1 > 0 ? ld32u(src + p + 2 - (int32_t)off1) : 0u;
+        }
+    };
+    int32_t pk = (int32_t)E[lane] - 256, pkN = (int32_t)E[64 + lane] - 256;
+    uint64_t v8 = 0;
+    uint32_t rw = 0;
+    loads(pk, v8, rw);
     for (uint32_t ci = 0;; ci += 64) {
         if (2 * (ci + 64) > kCertKeys) return false;  // too many keys: the exact search decides
-        const int32_t pk = (int32_t)E[ci + lane] - 256;
+        uint64_t v8N = 0;
+        uint32_t rwN = 0;
+        loads(pkN, v8N, rwN);
+        const int32_t pkNN = (int32_t)E[ci + 128 + lane] - 256;
         const bool valid = pk + 1 < ilimit;
         bool bad = false;
         if (valid) {
-            const uint64_t v8 = ld64u(src + pk);
-            bad = off1 > 0 && ld32u(src + pk + 2 - (int32_t)off1) == (uint32_t)(v8 >> 16);
+            bad = off1 > 0 && rw == (uint32_t)(v8 >> 16);
             const uint32_t h0 = z1::hash_word(v8, hlog, mls), h1 = z1::hash_word(v8 >> 8, hlog, mls);
             // ip0's key before ip1's: a lane's two keys are ordered too
             if (cert_insert(words, (uint32_t)v8 ^ (h0 * 0x9E3779B1u))) bad = true;
@@ -300,6 +314,10 @@ __device__ __noinline__ bool no_match_certificate(const uint8_t* __restrict__ sr
         }
         if (ballot(bad)) return false;
         if (ballot(!valid)) return true;  // the chain has left the block
+        pk = pkN;
+        pkN = pkNN;
+        v8 = v8N;
+        rw = rwN;
     }
 }
 
