@@ -1739,6 +1739,10 @@ struct pgn_ctx {
     // kernel of the neighbouring one; two per-chunk buffers alternate between sub-batches
     hipStream_t side = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr, evStage[2] = {nullptr, nullptr}, evFree[2] = {nullptr, nullptr};
+    // deferred-Huffman decode passes: the merges on a third stream, so the merge of pass p (VALU-bound)
+    // can share the CUs with the Huffman sections of pass p + 1 (latency-bound)
+    hipStream_t mergeS = nullptr;
+    hipEvent_t evHuf[2] = {nullptr, nullptr};
     uint64_t* prof = nullptr;  // [2][kPhases] phase cycles (encode, decode) when PGN_PHASE_PROFILE=1
     bool encTimed = false, decTimed = false;
     // Stream ordering of the context's shared state (work counters, slot scratch, per-chunk buffers):
@@ -1866,6 +1870,7 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
     HIPCHK(hipEventCreateWithFlags(&c->evLast, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->mergeS, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->scanStream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->evScanFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->evScan, hipEventDisableTiming));
@@ -1876,6 +1881,7 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     for (int i = 0; i < 2; i++) {
         HIPCHK(hipEventCreateWithFlags(&c->evStage[i], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&c->evFree[i], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->evHuf[i], hipEventDisableTiming));
     }
     // the predefined sequence FSE tables of the decoder (one wave, once per context)
     hipLaunchKernelGGL(seq_default_tables_kernel, dim3(1), dim3(64), 0, c->stream);
@@ -1915,10 +1921,13 @@ int pgn_ctx_destroy(pgn_ctx* c)
     if (c->scanStream) (void)hipStreamDestroy(c->scanStream);
     for (int i = 0; i < 4; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->side) (void)hipStreamSynchronize(c->side);
+    if (c->mergeS) (void)hipStreamSynchronize(c->mergeS);
     if (c->evLast) (void)hipEventSynchronize(c->evLast);
-    for (hipEvent_t e : {c->evFork, c->evJoin, c->evStage[0], c->evStage[1], c->evFree[0], c->evFree[1], c->evLast})
+    for (hipEvent_t e : {c->evFork, c->evJoin, c->evStage[0], c->evStage[1], c->evFree[0], c->evFree[1], c->evLast, c->evHuf[0],
+                         c->evHuf[1]})
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->mergeS) (void)hipStreamDestroy(c->mergeS);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return PGN_OK;
@@ -2317,15 +2326,23 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         if (defer)
             hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, sideS, a);
 #endif
-        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
+        // with deferred sections over several passes the merge goes to the third stream behind its
+        // pass's sections (so it overlaps the next pass's sections); the buffer is free after it
+        hipStream_t ms = sideS;
+        if (defer && passes > 1) {
+            HIPCHK(hipEventRecord(c->evHuf[b], c->side));
+            HIPCHK(hipStreamWaitEvent(c->mergeS, c->evHuf[b], 0));
+            ms = c->mergeS;
+        }
+        if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, ms, a);
         else if (a.lookback)  // few chunks: kMergeRanges single-wave workgroups per chunk
-            hipLaunchKernelGGL(dec_merge_lb_kernel, dim3((unsigned)(G * kMergeRanges)), dim3(64), 0, sideS, a);
-        else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, sideS, a);
-        if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], c->side));
+            hipLaunchKernelGGL(dec_merge_lb_kernel, dim3((unsigned)(G * kMergeRanges)), dim3(64), 0, ms, a);
+        else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, ms, a);
+        if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], ms));
     }
     HIPCHK(hipGetLastError());
-    if (passes > 1) {
-        HIPCHK(hipEventRecord(c->evJoin, c->side));
+    if (passes > 1) {  // the last merge follows every other launch of the call on the side streams
+        HIPCHK(hipEventRecord(c->evJoin, (defer && passes > 1) ? c->mergeS : c->side));
         HIPCHK(hipStreamWaitEvent(s, c->evJoin, 0));
     }
     return PGN_OK;
