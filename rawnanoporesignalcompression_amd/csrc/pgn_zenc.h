@@ -1100,57 +1100,62 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
     return maxNbBits;
 }
 
-// FSE_buildCTable_wksp for the weight alphabet (<= 13 symbols, tableLog <= 6), wave-uniform
+// FSE_buildCTable_wksp for the weight alphabet (<= 13 symbols, tableLog <= 6, so a table entry per
+// lane).  The serial spread visits positions (j * step) & mask for j = 0, 1, ... skipping those above
+// highThreshold, and the k-th accepted visit takes the k-th slot of the symbols in order; the state
+// table numbers each symbol's positions in increasing order (tableU16[cumul[s]++] = tableSize + u).
+// Both are computed lane-parallel here (visit j / entry u in lane j / u, ranks by ballot): the serial
+// loops were a chain of dependent LDS read-modify-writes, 64 per table.
 __device__ __forceinline__ void fse_build_ctable_small(WCTable& ct, const int16_t* norm, unsigned maxSymbolValue,
                                                        unsigned tableLog, uint8_t* tableSymbol, uint32_t* cumul)
 {
+    (void)cumul;
+    const uint32_t lane = (uint32_t)lane_id();
     const uint32_t tableSize = 1u << tableLog;
     const uint32_t tableMask = tableSize - 1;
     const uint32_t step = (tableSize >> 1) + (tableSize >> 3) + 3;
-    uint32_t highThreshold = tableSize - 1;
     ct.tableLog = tableLog;
-    cumul[0] = 0;
-    for (unsigned u = 1; u <= maxSymbolValue + 1; u++) {
-        if (norm[u - 1] == -1) {
-            cumul[u] = cumul[u - 1] + 1;
-            tableSymbol[highThreshold--] = (uint8_t)(u - 1);
-        } else {
-            cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
-        }
-    }
-    cumul[maxSymbolValue + 1] = tableSize + 1;
-    uint32_t position = 0;
-    for (unsigned symbol = 0; symbol <= maxSymbolValue; symbol++) {
-        const int freq = norm[symbol];
-        for (int k = 0; k < freq; k++) {
-            tableSymbol[position] = (uint8_t)symbol;
-            position = (position + step) & tableMask;
-            while (position > highThreshold) position = (position + step) & tableMask;
-        }
-    }
+    // symbol s in lane s: its count of positions (low-probability: 1) and the counts before it
+    const int nv = (lane <= maxSymbolValue) ? (int)norm[lane] : 0;
+    const bool low = nv == -1;
+    const uint32_t cnt = low ? 1u : (nv > 0 ? (uint32_t)nv : 0u);
+    const uint32_t excl = wave_incl_sum(cnt) - cnt;  // cumul[s]
+    // low-probability symbols at the top, in symbol order
+    const uint64_t lowMask = ballot(low);
+    if (low) tableSymbol[tableSize - 1 - mbcnt(lowMask)] = (uint8_t)lane;
+    const uint32_t highThreshold = tableSize - 1 - (uint32_t)__builtin_popcountll(lowMask);
+    // the spread: the other symbols' slots
+    const uint32_t ncnt = low ? 0u : cnt;
+    const uint32_t nincl = wave_incl_sum(ncnt);  // slots of the symbols <= s
+    const uint32_t pos = (lane * step) & tableMask;
+    const bool valid = lane < tableSize && pos <= highThreshold;
+    const uint32_t k = mbcnt(ballot(valid));  // this visit's slot
+    uint32_t sym = 0;
+    for (uint32_t q = 0; q <= maxSymbolValue; q++) sym += readlane_u32(nincl, (int)q) <= k ? 1u : 0u;
+    if (valid) tableSymbol[pos] = (uint8_t)sym;
     lds_sync();
-    for (uint32_t u = 0; u < tableSize; u++) {
-        const uint8_t sy = tableSymbol[u];
-        const uint32_t cs = cumul[sy];
-        ct.stateTable[cs] = (uint16_t)(tableSize + u);
-        cumul[sy] = cs + 1;
+    // the state table: entry u's symbol, its rank among that symbol's entries, the symbol's cumul
+    const bool isEntry = lane < tableSize;
+    const uint32_t sy = isEntry ? tableSymbol[lane] : 0xFFu;
+    uint32_t rank = 0;
+    for (uint32_t q = 0; q <= maxSymbolValue; q++) {
+        const uint64_t m = ballot(sy == q);
+        if (sy == q) rank = mbcnt(m);
     }
-    unsigned total = 0;
-    for (unsigned sy = 0; sy <= maxSymbolValue; sy++) {
-        const int nv = norm[sy];
+    const uint32_t cs = (uint32_t)__shfl((int)excl, (int)(sy & 63u), 64);
+    if (isEntry) ct.stateTable[cs + rank] = (uint16_t)(tableSize + lane);
+    if (lane <= maxSymbolValue) {
         if (nv == 0) {
-            ct.deltaNbBits[sy] = ((tableLog + 1) << 16) - (1u << tableLog);
-            ct.deltaFindState[sy] = 0;
+            ct.deltaNbBits[lane] = ((tableLog + 1) << 16) - (1u << tableLog);
+            ct.deltaFindState[lane] = 0;
         } else if (nv == -1 || nv == 1) {
-            ct.deltaNbBits[sy] = (tableLog << 16) - (1u << tableLog);
-            ct.deltaFindState[sy] = (int32_t)total - 1;
-            total++;
+            ct.deltaNbBits[lane] = (tableLog << 16) - (1u << tableLog);
+            ct.deltaFindState[lane] = (int32_t)excl - 1;
         } else {
             const uint32_t maxBitsOut = tableLog - z1::highbit32((uint32_t)(nv - 1));
             const uint32_t minStatePlus = (uint32_t)nv << maxBitsOut;
-            ct.deltaNbBits[sy] = (maxBitsOut << 16) - minStatePlus;
-            ct.deltaFindState[sy] = (int32_t)total - nv;
-            total += (unsigned)nv;
+            ct.deltaNbBits[lane] = (maxBitsOut << 16) - minStatePlus;
+            ct.deltaFindState[lane] = (int32_t)excl - nv;
         }
     }
     lds_sync();
