@@ -24,8 +24,7 @@
 
 namespace pgn {
 
-constexpr uint32_t kJobTab = 512;     // compact table slots of a job (16-bit: nbBits | symbol << 8)
-constexpr uint32_t kJobTabUse = 504;  // entries a table may have: dec_huf_kernel keeps 504 per frame in LDS
+// kJobTab / kJobTabUse: pgn_zdec.h (the table builder writes a job's compact table for dec_frame_fast)
 
 struct HufJob {
     uint64_t hp;      // the section's jump table; stream k starts at hp + 6 + len[0] + .. + len[k-1]
@@ -91,6 +90,27 @@ __device__ __forceinline__ bool huf_defer_body(uint8_t* job, unsigned tl, const 
         const uint32_t e = sDec.tab[j < T ? j : (j - Cc) << d];
         gst<uint16_t>(tab + j, (uint16_t)((e >> 8) | ((e & 0xFFu) << 8)));
     }
+    HufJob* J = (HufJob*)job;
+    if (lane == 0) {
+        gst<uint64_t>(&J->hp, (uint64_t)hp);
+        gst<uint64_t>(&J->dst, (uint64_t)dst);
+        gst<uint4>(&J->len[0], make_uint4(l1, l2, l3, l4));
+        gst<uint4>(&J->rs, make_uint4(rs, tl, K, Cc));
+        gst<uint32_t>(&J->flag, 1u);
+    }
+    return true;
+}
+// The job header alone (dec_frame_fast writes the compact table itself, from the table build's ranks):
+// the same checks and fields as huf_defer_body, K / Cc given.
+__device__ __forceinline__ bool huf_defer_header(uint8_t* job, unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst,
+                                                 uint32_t rs, uint32_t jt01, uint32_t jt2, uint32_t K, uint32_t Cc)
+{
+    const uint32_t lane = (uint32_t)lane_id();
+    const uint32_t l1 = jt01 & 0xFFFFu, l2 = jt01 >> 16, l3 = jt2;
+    if ((size_t)l1 + l2 + l3 + 6 > remain) return false;
+    const uint32_t l4 = (uint32_t)(remain - 6 - l1 - l2 - l3);
+    const uint32_t seg = (rs + 3) / 4;
+    if (seg * 3 > rs || tl < 1 || tl > kHufLdsLog) return false;
     HufJob* J = (HufJob*)job;
     if (lane == 0) {
         gst<uint64_t>(&J->hp, (uint64_t)hp);

@@ -18,6 +18,8 @@ constexpr int kSeqWin = 2048;            // sequences bitstream window staged in
 constexpr int kSeqHdr = 400;             // staged sequences-section header (table descriptions)
 constexpr int kSeqTab = 1280;            // LL [0,512) + OF [512,768) + ML [768,1280) FSE decode entries
 
+constexpr uint32_t kJobTab = 512;     // compact table slots of a deferred job (pgn_hufjob.h; 16-bit: nbBits | symbol << 8)
+constexpr uint32_t kJobTabUse = 504;  // entries a table may have: dec_huf_kernel keeps 504 per frame in LDS
 constexpr unsigned kHufLdsLog = 11;  // Huffman tables up to this log live in LDS (zstd's encoders
                                      // never exceed 11); a 12-bit table is built in HBM (slow path)
 
@@ -332,7 +334,8 @@ __device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxS
 // the description is staged from it (lane-permute reads, no memory round trip) when it lies inside
 __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
                                                        unsigned* minNbOut, const HdrWin* hw = nullptr, uint32_t hoff = 0,
-                                                       PhaseProf* Pp = nullptr)
+                                                       PhaseProf* Pp = nullptr, uint8_t* jobTab = nullptr,
+                                                       uint32_t* jobKC = nullptr)
 {
     const int lane = lane_id();
     src = uni(src);
@@ -503,6 +506,48 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
         if (sym < nbSym && w4[q]) sDec.order[before[w4[q]] + rankIdx[q]] = (uint8_t)sym;
     }
     lds_sync();
+    if (jobTab) {
+        // dec_frame_fast: the job's compact table (pgn_hufjob.h) straight from the ranks, without the
+        // 2^tl-entry table.  Entries with codes longer than K = tl - d are those of weights <= d, the
+        // first rankStart[d + 1] of the table; entry idx belongs to the last weight whose range starts
+        // at or below it.  A table above kJobTabUse entries returns 0: the caller's general path.
+        if (tl > kHufLdsLog) return 0;
+        const uint32_t tsz = 1u << tl;
+        uint32_t K = tl, T = 0, size = tsz;
+#pragma unroll
+        for (uint32_t d = 1; d <= 4; d++) {
+            if (d >= tl) break;
+            const uint32_t t = rankStart[d + 1], sz = t + ((tsz - t) >> d);
+            if (sz < size) {
+                size = sz;
+                K = tl - d;
+                T = t;
+            }
+        }
+        if (size > kJobTabUse) return 0;
+        const uint32_t d = tl - K, Cc = T - (T >> d);
+        for (uint32_t j = (uint32_t)lane; j < size; j += 64) {
+            const uint32_t idx = j < T ? j : (j - Cc) << d;
+            uint32_t w = 0, rs0 = 0, bf = 0;
+#pragma unroll
+            for (unsigned ww = 1; ww <= 12; ww++) {
+                const bool in = ww <= tl && cntW[ww] != 0 && rankStart[ww] <= idx;
+                w = in ? ww : w;
+                rs0 = in ? rankStart[ww] : rs0;
+                bf = in ? before[ww] : bf;
+            }
+            const uint32_t sym = sDec.order[bf + ((idx - rs0) >> (w - 1))];
+            gst<uint16_t>(jobTab + 2 * j, (uint16_t)((tl + 1 - w) | (sym << 8)));
+        }
+        jobKC[0] = K;
+        jobKC[1] = Cc;
+        *tlOut = tl;
+        uint32_t wmx = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) wmx = w4[q] > wmx ? w4[q] : wmx;
+        *minNbOut = tl + 1 - wave_max(wmx);
+        return used;
+    }
     // fill weight by weight: weight w owns entries [rankStart[w], rankStart[w] + cntW[w] << (w - 1))
 #pragma unroll
     for (unsigned w = 1; w <= 12; w++) {
@@ -1197,7 +1242,8 @@ __device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, 
     if (hw_byte(hw, src, ip + lh + cs) != 0) return -1;  // the sequences section: none
     const uint8_t* hp = src + ip + lh;
     unsigned tl = 0, mn = 1;
-    const size_t hsz = huf_build_dtable_body(hp, cs, &tl, htab, &mn, &hw, (uint32_t)(ip + lh), &P);  // (a 12-bit table goes to htab)
+    uint32_t kc[2] = {0, 0};
+    const size_t hsz = huf_build_dtable_body(hp, cs, &tl, htab, &mn, &hw, (uint32_t)(ip + lh), &P, job + sizeof(HufJob), kc);
     P.mark(1);
     if (hsz == 0 || tl > kHufLdsLog || cs - hsz < 6) return -1;
     hp += hsz;
@@ -1205,7 +1251,7 @@ __device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, 
     const size_t jp = (size_t)(hp - src);
     const uint32_t jt01 = hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16);
     const uint32_t jt2 = hw_u16(hw, src, jp + 4);
-    if (!huf_defer_body(job, tl, hp, remain, dst, (uint32_t)rs, jt01, jt2)) return -1;
+    if (!huf_defer_header(job, tl, hp, remain, dst, (uint32_t)rs, jt01, jt2, kc[0], kc[1])) return -1;
     return (long)rs;
 }
 
