@@ -30,9 +30,12 @@ typedef enum pgn_status {
     PGN_ERR_REMAINING = 4,        /* "Remaining data at end of signal buffer"       C5.hpp:675-677 */
     PGN_ERR_ZSTD_COMPRESS = 5,    /* "Failed to compress ..."                        C5.hpp:340-342 */
     PGN_ERR_CORRUPT = 6,          /* input on which the reference reads out of bounds (UB there) */
-    PGN_ERR_UNSUPPORTED = 9,      /* chunk above PGN_MAX_CHUNK_SAMPLES; decode: frames claiming more than 5 bytes
-                                     per sample of the call's largest chunk, rounded up to 4,096 samples (the
-                                     intermediate's capacity; calls of up to 64 chunks: 262,144 samples) */
+    PGN_ERR_ALLOC = 8,            /* decode: the frames' content sizes sum to more than 2^40 bytes, taken as the
+                                     reference's allocation of that intermediate failing (C5.hpp:575-583) */
+    PGN_ERR_UNSUPPORTED = 9,      /* chunk above PGN_MAX_CHUNK_SAMPLES; decode: frames claiming more content than
+                                     2.25 bytes per sample + 1,024 of the call's largest chunk (the intermediate's
+                                     capacity) that their blocks could really produce (a claim the blocks cannot
+                                     reach is "failed to decompress", as ZSTD_decompress reports it) */
     PGN_ERR_INVALID_ARG = 10,
     PGN_ERR_HIP = 11,             /* HIP runtime failure (message in pgn_last_error) */
     PGN_ERR_NO_DEVICE = 12,
@@ -47,9 +50,9 @@ typedef enum pgn_status {
  * chunk size is a writer option (c_api.h:526-539).
  * Chunks up to 262,144 samples run in the batched passes; larger ones in a second pass of the same
  * call whose per-chunk buffers are spaced for the largest of them (see the batch calls below).
- * Decode: a chunk's decoded frames share an intermediate buffer of 5 bytes per sample of the chunk
- * (a C5 chunk's streams take at most 3.75, an svb16 buffer 2.13 + 16 bytes); a blob whose frames
- * claim more content is PGN_ERR_UNSUPPORTED. */
+ * Decode: a chunk's decoded frames share an intermediate buffer of 2.25 bytes per sample + 1,024 of
+ * the call's largest chunk (262,144 samples when the call gives no bound): every blob whose frames
+ * decode to what its merge consumes fits it.  Frames claiming more: see PGN_ERR_UNSUPPORTED. */
 #define PGN_MAX_CHUNK_SAMPLES 16777216u
 
 /* Per-chunk statistics, the reference's global byte counters (src/c++/copy.cpp:64-85, updated at

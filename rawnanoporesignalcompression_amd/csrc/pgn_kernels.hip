@@ -110,12 +110,17 @@ __host__ __device__ inline DecLayout dec_layout()
     l.bytes = o;
     return l;
 }
-// A chunk's intermediate (the decoded frames back to back) holds 5 capN bytes: a C5 chunk's five
-// streams (<= 3.75 n), an svb16 buffer with its padding (<= 2.13 n + 16).
-__host__ __device__ constexpr size_t inter_cap(uint32_t capN) { return (size_t)5 * capN; }
+// A chunk's intermediate (the decoded frames back to back) holds 2.25 capN + 1,024 bytes: the most
+// any blob of a chunk of n <= capN samples holds when its frames decode to what its merge consumes --
+// C5 / C4: n/4 key bytes + 2 bytes per sample at most (a class-3 sample), every one of its S / M /
+// class-3 bytes standing for one sample; C1 / C2 / C3: n/8 + 2 n; VBZ0 n/4 + 2 n; VBZ's svb16 buffer
+// n/8 + 2 n + 16 padding bytes -- plus slack for trailing bytes ("Remaining data").  Frames claiming
+// more go through over_claim_status (the reference's own outcome for them, decided without decoding).
+__host__ __device__ constexpr size_t inter_cap(uint32_t capN) { return (size_t)capN * 9 / 4 + 1024; }
 // svb16::decode_input_buffer_padding_byte_count() on x86-64 (svb16/decode.hpp:16-23): the VBZ
 // intermediate is the frame content plus 16 bytes, and ZSTD_decompress may fill them.
 constexpr size_t kVbzPadding = 16;
+constexpr uint64_t kAllocLimit = (uint64_t)1 << 40;  // a decode intermediate above this is an allocation failure (PGN_ERR_ALLOC)
 __host__ __device__ constexpr size_t chunk_inter_bytes(uint32_t capN) { return align_up(inter_cap(capN) + 64, 256); }
 // per-chunk decode buffers of the two passes in flight (intermediates, records, Huffman jobs)
 constexpr size_t kDecBufferBudget = (size_t)24 << 30;
@@ -497,6 +502,24 @@ struct DecArgs {
     uint8_t* jobs;       // [G][5] HufJob records (pgn_hufjob.h): dec_zstd_kernel defers, dec_huf_kernel decodes; null = in place
 };
 
+// The status of a chunk whose frames claim more content (ZSTD_getFrameContentSize) than the
+// decoder's intermediate holds.  The reference allocates the sum of the claims (a size_t sum,
+// C5.hpp:575-583) and decompresses each frame into exactly its claim (C5.hpp:588-667): a sum above
+// 2^40 bytes is taken as that allocation failing (PGN_ERR_ALLOC, as the oracle), a frame whose blocks
+// cannot produce its claim fails in ZSTD_decompress ("failed to decompress", PGN_ERR_ZSTD_DECOMPRESS,
+// z1::frame_content_bound); only frames that could really expand that far are PGN_ERR_UNSUPPORTED.
+__device__ inline int over_claim_status(const uint8_t* in, const DecUnit* u, const uint64_t* cs, int nf)
+{
+    uint64_t tot = 0;
+    for (int s = 0; s < nf; s++) tot += cs[s];
+    if (tot > kAllocLimit) return PGN_ERR_ALLOC;
+    for (int s = 0; s < nf; s++) {
+        const int64_t b = z1::frame_content_bound(in + u[s].src, (size_t)u[s].len);
+        if (b < 0 || (uint64_t)b < cs[s]) return PGN_ERR_ZSTD_DECOMPRESS;
+    }
+    return PGN_ERR_UNSUPPORTED;
+}
+
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586).
 // Frames claiming more content than the intermediate holds (interCap = 5 capN bytes, capN >= every
 // chunk of the call) or a stream above kPassSamples are PGN_ERR_UNSUPPORTED (include/pgnano_hip.h).
@@ -524,7 +547,7 @@ __device__ inline int c5_parse_chunk(const uint8_t* in, uint64_t src0, uint64_t 
     }
     uint64_t off = 0;
     for (int s = 0; s < kStreams; s++) {
-        if (cs[s] > kPassSamples || cs[s] > interCap - off) return PGN_ERR_UNSUPPORTED;
+        if (cs[s] > kPassSamples || cs[s] > interCap - off) return over_claim_status(in, u, cs, kStreams);
         u[s].cs = (uint32_t)cs[s];
         u[s].interOff = (uint32_t)off;
         off += cs[s];
@@ -671,6 +694,11 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     const uint32_t flag = inb ? gld<uint32_t>(&J->flag) : 0u;
     const uint64_t fm = ballot(flag != 0);
     if (fm == 0) return;
+    // phase profile build: dec_huf's own region of the profile buffer (kHufProfOff, DecArgs.prof = +kPhases)
+    PhaseProf Pp;
+    Pp.init(a.prof ? a.prof + (kHufProfOff - kPhases) : nullptr);
+    Pp.count(0);
+    Pp.count(2, (uint64_t)__builtin_popcountll(fm));
     // the pending frames' compact tables (kTabStride entries each, 16 bytes per lane; all loads in
     // flight at once)
     {
@@ -687,6 +715,7 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
         if (lane < kZeroTab / 2) ((uint32_t*)&tabs[kHufFrames * kTabStride])[lane] = 0u;
     }
     uint8_t* const junk = a.jobs + G * kStreams * kJobBytes + 128 * lane;
+    Pp.mark(0);  // the job flags and the compact tables in LDS
     // this lane's stream
     uint64_t hp = 0, dstp = 0;
     uint4 len = make_uint4(0, 0, 0, 0), prm = make_uint4(0, 11, 11, 0);
@@ -880,6 +909,9 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     // trips of 8 iterations: one whole line per lane
     const int lines = nD > (int)m0 ? (nD - (int)m0 + 7) / 8 : 0;
     const int trips = (int)wave_max((uint32_t)lines);
+    Pp.mark(1);  // stream setup, first loads, the 8-iteration prologue
+    Pp.count(1, (uint64_t)trips);
+    Pp.count(3, (uint64_t)wave_sum(nsym));
     for (int t = 0; t < trips; t++) {
         uint4 Dk[8];
 #pragma unroll
@@ -895,6 +927,7 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
             gst<uint4>(ad, Dk[k]);
         }
     }
+    Pp.mark(2);  // the trips of 8 iterations
 #pragma unroll
     for (uint32_t k = 0; k < kPf; k++) {
         stage(lb[k], La[k]);
@@ -920,6 +953,8 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     if (live) bad = (v0 + 32u * (ins - ins0) - avail) != totalBits;
     const uint64_t bm = ballot(bad);
     if (q == 0 && flag && ((bm >> (4 * f)) & 0xFull)) gst<int32_t>(&a.units[g * kStreams + (size_t)s].dres, (int32_t)z1::kDecErrHufStream);
+    Pp.mark(3);  // drain, head / tail bytes, the last symbols, the end check
+    Pp.flush();
 }
 
 // Small batches (the per-chunk calls): one workgroup of kCoopWaves waves per work unit.  Wave 0
@@ -1175,8 +1210,12 @@ __global__ __launch_bounds__(64) void vbz_parse_kernel(DecArgs a)
     int st = PGN_OK;
     if (a.sampleCounts[c] > kPassSamples) st = PGN_ERR_UNSUPPORTED;  // the large-chunk pass takes it
     else if (!ok) st = PGN_ERR_NOT_ZSTD;
-    else if (cs + kVbzPadding > inter_cap(a.capN) || len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
-    else {
+    else if (len > 0xFFFFFFFFull) st = PGN_ERR_UNSUPPORTED;
+    else if (cs + kVbzPadding > inter_cap(a.capN)) {
+        u->src = src0;
+        u->len = (uint32_t)len;
+        st = over_claim_status(a.in, u, &cs, 1);
+    } else {
         u->src = src0;
         u->len = (uint32_t)len;
         u->cs = (uint32_t)cs;
@@ -1496,7 +1535,7 @@ __device__ inline int parse_frames(const uint8_t* in, uint64_t src0, uint64_t le
     }
     uint64_t off = 0;
     for (int s = 0; s < NF; s++) {
-        if (cs[s] > interCap - kVbzPadding - off) return PGN_ERR_UNSUPPORTED;
+        if (cs[s] > interCap - kVbzPadding - off) return over_claim_status(in, u, cs, NF);
         u[s].cs = (uint32_t)cs[s];
         u[s].interOff = (uint32_t)off;
         off += cs[s];
@@ -1539,9 +1578,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
                           : __builtin_amdgcn_readfirstlane(
                                 parse_frames<nf>(a.in, a.inOffsets[c], a.inSizes[c], d, &total, inter_cap(capN)));
         if (Codec == kCodecC5 && st == PGN_OK) {  // C5: the staged path's per-stream bound
+            uint64_t cs64[kStreams];
+            bool over = false;
 #pragma unroll
-            for (int s = 0; s < nf; s++)
-                if (d[s].cs > capN) st = PGN_ERR_UNSUPPORTED;
+            for (int s = 0; s < nf; s++) {
+                cs64[s] = d[s].cs;
+                over = over || d[s].cs > capN;
+            }
+            if (over) st = __builtin_amdgcn_readfirstlane(over_claim_status(a.in, d, cs64, nf));
         }
         if (st == PGN_OK) {
 #pragma unroll
@@ -1743,7 +1787,7 @@ struct pgn_ctx {
     // can share the CUs with the Huffman sections of pass p + 1 (latency-bound)
     hipStream_t mergeS = nullptr;
     hipEvent_t evHuf[2] = {nullptr, nullptr};
-    uint64_t* prof = nullptr;  // [2][kPhases] phase cycles (encode, decode) when PGN_PHASE_PROFILE=1
+    uint64_t* prof = nullptr;  // kProfWords: phase cycles and counters (encode, decode, dec_huf) when PGN_PHASE_PROFILE=1
     bool encTimed = false, decTimed = false;
     // Stream ordering of the context's shared state (work counters, slot scratch, per-chunk buffers):
     // every launch sequence records evLast on its stream at the end, and the next one, on whatever
@@ -1797,7 +1841,8 @@ const char* pgn_status_string(int s)
     case PGN_ERR_REMAINING: return "Remaining data at end of signal buffer";
     case PGN_ERR_ZSTD_COMPRESS: return "Failed to compress data";
     case PGN_ERR_CORRUPT: return "Corrupt compressed signal (stream read past its end)";
-    case PGN_ERR_UNSUPPORTED: return "Chunk larger than PGN_MAX_CHUNK_SAMPLES";
+    case PGN_ERR_ALLOC: return "Out of memory: the frames' content sizes sum to more than 2^40 bytes";
+    case PGN_ERR_UNSUPPORTED: return "Chunk larger than PGN_MAX_CHUNK_SAMPLES, or frames expanding beyond the decoder's buffer";
     case PGN_ERR_INVALID_ARG: return "Invalid argument";
     case PGN_ERR_HIP: return "HIP runtime error";
     case PGN_ERR_NO_DEVICE: return "No HIP device";
@@ -1863,8 +1908,8 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     const char* pe = getenv("PGN_PHASE_PROFILE");
     if (pe && pe[0] == '1') {
         // [encode phases][decode phases][encode counters][decode counters]
-        HIPCHK(hipMalloc(&c->prof, 2 * (kPhases + kCounters) * sizeof(uint64_t)));
-        HIPCHK(hipMemset(c->prof, 0, 2 * (kPhases + kCounters) * sizeof(uint64_t)));
+        HIPCHK(hipMalloc(&c->prof, kProfWords * sizeof(uint64_t)));
+        HIPCHK(hipMemset(c->prof, 0, kProfWords * sizeof(uint64_t)));
         HIPCHK(hipDeviceSynchronize());
     }
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
@@ -2542,17 +2587,11 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
     if (c->haveLast) HIPCHK(hipStreamWaitEvent(s, c->evLast, 0));
     const bool scan = need_scan(maxHint);
-    // The intermediates are spaced for the call's largest chunk.  Large C5 batches (the deferred
-    // Huffman path, many chunks per pass) read it from the scan before launching; the others keep
-    // kPassSamples when the caller gives no bound (the scan then runs beside the batched pass).
-    const bool early = scan && codec == kCodecC5 && c->decStaged && nchunks >= c->deferMin;
+    // The intermediates are spaced for the call's largest chunk when the caller bounds it, else for
+    // kPassSamples (the scan then runs beside the batched pass, and the launch stays asynchronous).
     uint32_t capCall = (!scan && maxHint) ? call_cap(maxHint) : kPassSamples;
-    uint32_t count = 0, maxN = 0, maxAll = 0;
+    uint32_t count = 0, maxN = 0;
     int rc = scan ? start_scan(c, nchunks, d_sample_counts, s) : PGN_OK;
-    if (rc == PGN_OK && early) {
-        rc = finish_scan(c, count, maxN, &maxAll);
-        capCall = call_cap(maxAll);
-    }
     // small calls (the per-chunk ones) keep the full capacity: a frame is then decoded up to its own
     // content size, as the reference does, and the chunk ends with its statuses (e.g. "Remaining
     // data" for samples fewer than the frames hold) rather than PGN_ERR_UNSUPPORTED
@@ -2560,7 +2599,7 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     if (rc == PGN_OK)
         rc = launch_decode_impl(c, codec, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                                 d_sample_counts, d_status, s, capCall);
-    if (rc == PGN_OK && scan && !early) rc = finish_scan(c, count, maxN);
+    if (rc == PGN_OK && scan) rc = finish_scan(c, count, maxN);
     if (rc == PGN_OK && count)
         rc = launch_large_decode(c, codec, count, maxN, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                                  d_sample_counts, d_status, s);
@@ -2718,7 +2757,7 @@ int pgn_debug_huf_dump(uint32_t* out, size_t nwords)
 int pgn_debug_phase_cycles(pgn_ctx* c, uint64_t* out, int n)
 {
     if (!c || !out || n < 2 * kPhases) return PGN_ERR_INVALID_ARG;
-    const int m = n < 2 * (kPhases + kCounters) ? n : 2 * (kPhases + kCounters);
+    const int m = n < kProfWords ? n : kProfWords;
     if (!c->prof) {
         memset(out, 0, sizeof(uint64_t) * m);
         return PGN_OK;

@@ -208,6 +208,10 @@ __device__ inline void wave_fill(uint8_t* dst, uint8_t v, size_t n)
 // ---------------------------------------------------------------------------------------------
 constexpr int kPhases = 16;
 constexpr int kCounters = 16;  // event counters (loop trip counts) after the phase cycles
+// profile buffer: [encode phases][decode phases][encode counters][decode counters], then the same
+// pair for dec_huf_kernel (phases at kHufProfOff, counters 2 kPhases further on)
+constexpr int kHufProfOff = 2 * (kPhases + kCounters);
+constexpr int kProfWords = kHufProfOff + 2 * (kPhases + kCounters);
 struct PhaseProf {
 #ifdef PGN_PROFILE
     uint64_t* out;

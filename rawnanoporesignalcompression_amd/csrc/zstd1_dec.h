@@ -61,6 +61,75 @@ PGN_HD uint64_t frame_content_size(const uint8_t* src, size_t n, bool* ok)
     return v;
 }
 
+// An upper bound on the bytes ZSTD_decompress can produce from the first frame of src[0, n): the
+// frame's blocks are walked by their headers -- a raw or RLE block its size, a compressed block the
+// regenerated size of its literals when its sequence count is 0, else ZSTD_BLOCKSIZE_MAX (128 KiB).
+// -1: the first frame cannot decode at all (not a frame, a reserved block type, a block past n),
+// which libzstd reports as an error.  A skippable frame produces nothing.  Used only for frames whose
+// content size claims more than the decoder's buffers hold: a claim above the bound fails the
+// frame-content-size check of ZSTD_decompress (or the frame fails before it), whatever follows.
+PGN_HD int64_t frame_content_bound(const uint8_t* src, size_t n)
+{
+    if (n < 5) return -1;
+    const uint32_t magic = rd32(src);
+    if ((magic & 0xFFFFFFF0u) == 0x184D2A50u) return 0;
+    if (magic != kMagic) return -1;
+    const uint8_t fhd = src[4];
+    const unsigned dictIDFlag = fhd & 3, singleSegment = (fhd >> 5) & 1, fcsFlag = fhd >> 6;
+    const unsigned didSize[4] = {0, 1, 2, 4};
+    const unsigned fcsSize = (fcsFlag == 0) ? (singleSegment ? 1 : 0) : (1u << fcsFlag);
+    size_t pos = 5 + !singleSegment + didSize[dictIDFlag] + fcsSize;
+    if (pos > n) return -1;
+    int64_t bound = 0;
+    while (true) {
+        if (n - pos < 3) return -1;
+        const uint32_t bh = (uint32_t)src[pos] | ((uint32_t)src[pos + 1] << 8) | ((uint32_t)src[pos + 2] << 16);
+        pos += 3;
+        const uint32_t type = (bh >> 1) & 3u, bsize = bh >> 3;
+        if (type == 3) return -1;
+        if (type == 1) {  // RLE: one byte, bsize copies
+            if (n - pos < 1) return -1;
+            pos += 1;
+            bound += bsize;
+        } else {
+            if (n - pos < bsize) return -1;
+            if (type == 0) {
+                bound += bsize;
+            } else {  // compressed: literals header (RFC 8878 3.1.1.3.1.1), then the sequence count byte
+                const uint8_t* b = src + pos;
+                int64_t cb = 131072;
+                if (bsize >= 1) {
+                    const uint32_t lt = b[0] & 3u, sf = (b[0] >> 2) & 3u;
+                    uint32_t lh = 0, regen = 0, comp = 0;
+                    if (lt < 2) {
+                        lh = sf == 1 ? 2 : (sf == 3 ? 3 : 1);
+                        if (bsize >= lh) {
+                            regen = sf == 1 ? (b[0] >> 4) + ((uint32_t)b[1] << 4)
+                                            : (sf == 3 ? (b[0] >> 4) + ((uint32_t)b[1] << 4) + ((uint32_t)b[2] << 12) : (uint32_t)b[0] >> 3);
+                            comp = lt == 0 ? regen : 1u;
+                        }
+                    } else {
+                        lh = sf < 2 ? 3 : (sf == 2 ? 4 : 5);
+                        if (bsize >= lh) {
+                            uint64_t h = 0;
+                            for (uint32_t k = 0; k < lh; k++) h |= (uint64_t)b[k] << (8 * k);
+                            const uint32_t w = sf < 2 ? 10 : (sf == 2 ? 14 : 18);
+                            regen = (uint32_t)((h >> 4) & ((1u << w) - 1u));
+                            comp = (uint32_t)((h >> (4 + w)) & ((1u << w) - 1u));
+                        }
+                    }
+                    const uint64_t sec = (uint64_t)lh + comp;
+                    if (lh && bsize >= lh && sec < bsize && b[sec] == 0) cb = regen;  // no sequences: the literals
+                }
+                bound += cb;
+            }
+            pos += bsize;
+        }
+        if (bh & 1u) break;
+    }
+    return bound;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Backward bit reader (BIT_DStream semantics: the last byte's highest set bit is the end mark;
 // bits below position 0 read as zero and flag an overrun).

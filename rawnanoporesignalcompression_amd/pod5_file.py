@@ -303,12 +303,17 @@ def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", varia
     its batches with one batched decode and one batched encode on its GPU.  Then the collectives
     carry sizes only (BASELINE north_star: RCCL for the size reduction): an all-gather of (status,
     counts) and one of the rows' compressed sizes.  From them every rank computes the same file
-    layout (pgn_pod5_write_file_reserved); rank 0 writes the file with the signal bytes left zero,
-    and every rank writes its own rows' bytes in place (positioned writes).  The file is byte for
-    byte what the one-rank call writes.  A failure on any rank -- also before the first collective
-    (opening the file, creating the codec) -- raises on every rank, and no rank waits on a collective
-    another rank never reaches.  Returns the whole job's stats on every rank (decode_ms / encode_ms:
-    the slowest rank's).  `_part` replaces the GPU share (tests on CPU)."""
+    layout (pgn_pod5_write_file_reserved); rank 0 writes it, with the signal bytes left zero, under a
+    temporary name beside out_path (`<out_path>.pgn-tmp-<token>`, the token in the first gather) and
+    shares the file's 16-byte section marker; every rank checks the marker at offset 8 of that file
+    before it writes its own rows' bytes in place (positioned writes), so no rank writes into a stale
+    file of the same name.  Only when every rank has written does rank 0 rename the file to out_path;
+    on any failure it is removed and out_path is left as it was.  The file is byte for byte what the
+    one-rank call writes.  out_path must be on a filesystem every rank sees.  A failure on any rank --
+    also before the first collective (opening the file, creating the codec) -- raises on every rank,
+    and no rank waits on a collective another rank never reaches.  Returns the whole job's stats on
+    every rank (decode_ms / encode_ms: the slowest rank's).  `_part` replaces the GPU share (tests on
+    CPU)."""
     import os
 
     import torch
@@ -321,7 +326,7 @@ def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", varia
     if device is None:
         device = int(os.environ.get("LOCAL_RANK", rank))
     nccl = dist.get_backend(group) == "nccl"
-    f, own = None, False
+    f, own, made, tmp_path = None, False, False, None
     status, msg, counts, times, offs, data = 0, "", [0, 0, 0, 0], [0.0, 0.0], None, None
     try:
         dev = torch.device("cuda", device) if nccl else torch.device("cpu")
@@ -345,13 +350,16 @@ def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", varia
         except Exception as e:  # noqa: BLE001 -- reported to every rank below
             status = int(getattr(e, "status", 0) or PGN_ERR_IO)
             msg = f"{type(e).__name__}: {e}"
-        # ---- sizes 1: status and counts of every rank
-        head = torch.tensor([status] + [int(v) for v in counts], dtype=torch.int64, device=dev)
+        # ---- sizes 1: status and counts of every rank (and rank 0's temporary-file token)
+        token = int.from_bytes(os.urandom(7), "little") if rank == 0 else 0
+        head = torch.tensor([status] + [int(v) for v in counts] + [token], dtype=torch.int64, device=dev)
         heads = [torch.empty_like(head) for _ in range(world)]
         dist.all_gather(heads, head, group=group)
         tm = torch.tensor(times, dtype=torch.float64, device=dev)
         dist.all_reduce(tm, op=dist.ReduceOp.MAX, group=group)
         heads = torch.stack(heads).cpu().numpy()
+        tmp_path = f"{out_path}.pgn-tmp-{int(heads[0, -1]):014x}"
+        heads = heads[:, :-1]
         bad = [(r, int(heads[r, 0])) for r in range(world) if heads[r, 0]]
         if bad:
             r, s = bad[0]
@@ -372,41 +380,81 @@ def transcode_pod5_ranks(in_path: str, out_path: str, dst: str = "pgnano", varia
         pos = np.zeros(f.rows, np.uint64)
         lib = _native.load()
         err = None
+        marker = bytes(16)
         if rank == 0:
-            rc = lib.pgn_pod5_write_file_reserved(str(out_path).encode(), f._h, SIGNAL_TYPES[dst], f.rows, _ptr(ids),
+            made = True
+            rc = lib.pgn_pod5_write_file_reserved(tmp_path.encode(), f._h, SIGNAL_TYPES[dst], f.rows, _ptr(ids),
                                                   _ptr(samples), offs_all.ctypes.data, int(rows_per_batch), None,
                                                   None, 1, _ptr(pos))
             if rc:
                 err = Pod5FileError(rc, f"write {out_path}")
+            else:
+                try:
+                    marker = _section_marker(tmp_path)
+                except OSError as e:
+                    err = Pod5FileError(PGN_ERR_IO, f"read back {tmp_path}: {e}")
         else:
             rc = lib.pgn_pod5_write_file_reserved(None, f._h, SIGNAL_TYPES[dst], f.rows, _ptr(ids), _ptr(samples),
                                                   offs_all.ctypes.data, int(rows_per_batch), None, None, 0, _ptr(pos))
             if rc:
                 err = Pod5FileError(rc, f"layout of {out_path}")
-        flag = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        # the layout's outcome on every rank, and rank 0's section marker (two int64 words)
+        mk = np.frombuffer(marker, np.int64)
+        flag = torch.tensor([0 if err is None else 1, int(mk[0]), int(mk[1])], dtype=torch.int64, device=dev)
+        flags = [torch.empty_like(flag) for _ in range(world)]
+        dist.all_gather(flags, flag, group=group)
+        flags = torch.stack(flags).cpu().numpy()
         if err is not None:
             raise err
-        if int(flag.item()):
+        if flags[:, 0].any():
             raise Pod5FileError(PGN_ERR_IO, f"another rank failed to lay out {out_path}")
+        marker = flags[0, 1:].astype(np.int64).tobytes()
         # ---- every rank writes its own rows in place, then all agree that the file is complete
         try:
-            _write_rows_at(out_path, pos, sizes, runs, offs, data)
+            _write_rows_at(tmp_path, pos, sizes, runs, offs, data, marker)
         except OSError as e:
-            err = Pod5FileError(PGN_ERR_IO, f"rank {rank}: positioned write to {out_path}: {e}")
+            err = Pod5FileError(PGN_ERR_IO, f"rank {rank}: positioned write to {tmp_path}: {e}")
         flag = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
         if err is not None:
             raise err
         if int(flag.item()):
             raise Pod5FileError(PGN_ERR_IO, f"another rank failed to write its rows of {out_path}")
+        # ---- the complete file takes its name; every rank returns once it has
+        if rank == 0:
+            try:
+                os.replace(tmp_path, out_path)
+                made = False
+            except OSError as e:
+                err = Pod5FileError(PGN_ERR_IO, f"rename {tmp_path} -> {out_path}: {e}")
+        flag = torch.tensor([0 if err is None else 1], dtype=torch.int64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if err is not None:
+            raise err
+        if int(flag.item()):
+            raise Pod5FileError(PGN_ERR_IO, f"rank 0 failed to rename the finished {out_path}")
         tot = heads[:, 1:].sum(axis=0)
         return _stats_dict(int(tot[0]), int(tot[1]), int(tot[2]), int(tot[3]), float(tm[0]), float(tm[1]))
     finally:
+        if made:  # rank 0, the file never completed: no partial file stays behind
+            try:
+                os.unlink(tmp_path)
+            except OSError:
+                pass
         if own:
             codec.close()
         if f is not None:
             f.close()
+
+
+def _section_marker(path: str) -> bytes:
+    """The 16-byte section marker after the 8-byte signature of a combined POD5 file."""
+    with open(path, "rb") as fh:
+        fh.seek(8)
+        b = fh.read(16)
+    if len(b) != 16:
+        raise OSError(f"{path}: no section marker")
+    return b
 
 
 def _merge_sizes(f: Pod5File, parts, nrow, world: int, rank: int):
@@ -429,12 +477,15 @@ def _merge_sizes(f: Pod5File, parts, nrow, world: int, rank: int):
     return sizes, runs
 
 
-def _write_rows_at(path: str, pos, sizes, runs, offs, data) -> None:
-    """This rank's rows at their file positions, one write per stretch that is contiguous in the file."""
+def _write_rows_at(path: str, pos, sizes, runs, offs, data, marker: bytes | None = None) -> None:
+    """This rank's rows at their file positions, one write per stretch that is contiguous in the file.
+    With `marker`, the file must carry that section marker at offset 8 (the file rank 0 laid out)."""
     import os
 
-    fd = os.open(str(path), os.O_WRONLY)
+    fd = os.open(str(path), os.O_RDWR)
     try:
+        if marker is not None and os.pread(fd, 16, 8) != marker:
+            raise OSError(f"{path} is not the file laid out for this copy (section marker differs)")
         for row0, p0, n in runs:
             i = 0
             while i < n:

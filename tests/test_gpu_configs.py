@@ -135,3 +135,82 @@ def test_one_context_two_streams(codec):
     for r in list(range(0, k, 61)) + [k - 1]:
         ref = O.c5_compress(O.synth_read(r, n))[1]
         assert b0[bo_h[r]:bo_h[r] + bs_h[r]].tobytes() == ref, r
+
+
+def _deferred_codec(min_chunks: str, group: str):
+    import os
+
+    from rawnanoporesignalcompression_amd import PGNanoCodec
+
+    keys = ("PGN_DEFER_MIN_CHUNKS", "PGN_DEFER_G")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ["PGN_DEFER_MIN_CHUNKS"], os.environ["PGN_DEFER_G"] = min_chunks, group
+    try:
+        return PGNanoCodec(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_mixed_pore_decode_only_deferred_path():
+    """configs[4]'s corpus through the production decode path of large batches (the deferred
+    four-stream Huffman sections, dec_huf_kernel) in passes of 48 chunks (both pass buffers, three
+    passes): oracle-made blobs of every chemistry, samples equal to the oracle's reads."""
+    import torch
+
+    n, per = 100_000, 40
+    xs, blobs = [], []
+    for i, pq in enumerate(PORES.values()):
+        for r in range(per):
+            x = O.synth_read(1000 * i + r, n, p_switch_q16=pq)
+            rc, b, _ = O.c5_compress(x)
+            assert rc == 0
+            xs.append(x)
+            blobs.append(b)
+    flat, offs, sizes = _flat(blobs)
+    counts = np.full(len(xs), n, np.int32)
+    dev = torch.device("cuda", 0)
+    c = _deferred_codec("1", "48")
+    try:
+        out, _, st = c.decompress_batch(torch.from_numpy(flat).to(dev), torch.from_numpy(offs).to(dev),
+                                        torch.from_numpy(sizes).to(dev), torch.from_numpy(counts).to(dev))
+        torch.cuda.synchronize()
+        assert "dec_huf_kernel" in c.kernels(1)
+    finally:
+        c.close()
+    assert (st.cpu().numpy() == 0).all()
+    assert np.array_equal(out.cpu().numpy(), np.concatenate(xs))
+
+
+def test_mixed_pore_decode_at_production_defaults(codec):
+    """configs[4] at the default thresholds: 12,600 mixed-chemistry chunks (above PGN_DEFER_MIN_CHUNKS
+    = 12,288, so the deferred path the configs[4] bench line runs), encoded on the GPU (sampled blobs
+    equal to the oracle's) and decoded back exactly."""
+    import torch
+
+    n, k = 100_000, 12600
+    dev = torch.device("cuda", 0)
+    samples = torch.empty(k * n, dtype=torch.int16, device=dev)
+    cuts = [0, k // 3, 2 * k // 3, k]
+    pqs = list(PORES.values())
+    for i, pq in enumerate(pqs):
+        a, e = cuts[i], cuts[i + 1]
+        codec.synth_reads(e - a, n, seed=42, first_read=a, p_switch_q16=pq, out=samples[a * n:e * n])
+    offs = torch.arange(k, dtype=torch.int64, device=dev) * n
+    cnt = torch.full((k,), n, dtype=torch.int32, device=dev)
+    enc = codec.compress_batch(samples, offs, cnt)
+    out, _, st = codec.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
+    torch.cuda.synchronize()
+    assert "dec_huf_kernel" in codec.kernels(1)
+    assert (enc.status == 0).all() and (st == 0).all()
+    assert torch.equal(out, samples)
+    blobs, bo, bs = enc.blobs, enc.offsets.cpu().numpy(), enc.sizes.cpu().numpy()
+    for r in (0, 1, k // 3 - 1, k // 3, 2 * k // 3 + 7, k - 1):
+        i = 0 if r < cuts[1] else (1 if r < cuts[2] else 2)
+        x = O.synth_read(r, n, p_switch_q16=pqs[i])
+        assert np.array_equal(samples[r * n:(r + 1) * n].cpu().numpy(), x), r
+        rc, ref, _ = O.c5_compress(x)
+        assert rc == 0 and blobs[bo[r]:bo[r] + bs[r]].cpu().numpy().tobytes() == ref, r

@@ -5,7 +5,9 @@ Large decode batches take this path (PGN_DEFER_MIN_CHUNKS, default 12,288 chunks
 made with the threshold at 1 chunk and passes of 96 chunks, so that small batches run it: mixed chunk
 sizes (every alignment of the streams' destinations, short last streams, several passes with both
 buffers), the Huffman stress shapes (1-bit to 11-bit codes), corrupted blobs (statuses equal to the
-oracle's, the known X2-tail divergence of DESIGN §3 aside) and full-size chunks.
+oracle's, the known X2-tail divergence of DESIGN §3 aside; frame headers corrupted to claim more content
+than the intermediate holds get the reference's status too: PGN_ERR_ZSTD_DECOMPRESS, or PGN_ERR_ALLOC
+past 2^40 bytes) and full-size chunks.
 """
 import os
 
@@ -101,35 +103,6 @@ def test_deferred_decode_huffman_stress_shapes(dcodec):
         assert np.array_equal(got[i], x), i
 
 
-def _claims_too_much(blob: bytes, n: int) -> bool:
-    """The frames' content sizes exceed the decoder's documented bound (include/pgnano_hip.h,
-    PGN_ERR_UNSUPPORTED: more than 5 bytes per sample, or a stream above 262,144 bytes)."""
-    import ctypes as C
-    import struct
-
-    m = O.model()
-    pos, tot = 0, 0
-    for s in range(5):
-        if s < 4:
-            if pos + 8 > len(blob):
-                return False
-            fl = struct.unpack_from("<Q", blob, pos)[0]
-            pos += 8
-        else:
-            fl = len(blob) - pos
-        if fl > len(blob) - pos:
-            return False
-        fr = np.frombuffer(blob[pos:pos + fl], np.uint8).copy()
-        cs = m.z1m_content_size(fr.ctypes.data_as(C.c_void_p), C.c_size_t(fl)) if fl else -1
-        if cs < 0:
-            return False
-        if cs > 262144:
-            return True
-        tot += cs
-        pos += fl
-    return tot > 5 * n
-
-
 def test_deferred_decode_corrupted_statuses_equal_oracle(dcodec):
     rng = np.random.default_rng(7)
     lens = list(rng.integers(2000, 102401, 160))
@@ -149,8 +122,6 @@ def test_deferred_decode_corrupted_statuses_equal_oracle(dcodec):
         rc, ref = O.c5_decompress(b, int(lens[i]))
         if rc == 0 and st[i] == 3 and not O.c5_frames_strictly_valid(b):
             continue  # libzstd's double-symbol decoder accepts one trailing codeword
-        if st[i] == 9 and _claims_too_much(b, int(lens[i])):
-            continue  # a corrupted frame header claims more content than the documented bound
         assert st[i] == rc, (i, rc, st[i])
         if rc == 0:
             assert np.array_equal(got[i], ref), i

@@ -1,0 +1,141 @@
+"""Frames whose content sizes claim more than the decoder's intermediate holds (2.25 bytes per sample
++ 1,024 of the call's largest chunk): the statuses the reference reaches on them, through the per-chunk
+path, a small batch and the large-batch (deferred Huffman) path.
+
+The reference allocates the sum of the claims and decompresses each frame into exactly its claim
+(C5.hpp:575-667).  A claim the frame's blocks cannot produce fails the frame-content-size check of
+ZSTD_decompress: "failed to decompress" (3).  A sum above 2^40 bytes is an allocation failure (8, as the
+oracle).  A frame that really expands past the buffer (an RLE block of 300,000 zero bytes) decodes under
+the reference and its chunk ends in "Remaining data" (4); the GPU path reports PGN_ERR_UNSUPPORTED (9)
+for it -- the one documented divergence (include/pgnano_hip.h), pinned here.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+
+def _frames(x):
+    return [O.zstd_compress1(s) for s in O.c5_streams(x)]
+
+
+def _set_fcs(frame: bytes, value: int) -> bytes:
+    """The frame with an 8-byte content-size field holding `value` (single-segment frame header)."""
+    assert frame[:4] == b"\x28\xb5\x2f\xfd"
+    fhd = frame[4]
+    assert (fhd >> 5) & 1  # single segment (libzstd level 1 on these streams)
+    fcs_size = {0: 1, 1: 2, 2: 4, 3: 8}[fhd >> 6]
+    did = {0: 0, 1: 1, 2: 2, 3: 4}[fhd & 3]
+    body = frame[5 + did + fcs_size:]
+    return frame[:4] + bytes([(fhd & 0x3F) | 0xC0]) + frame[5:5 + did] + struct.pack("<Q", value) + body
+
+
+def _cases():
+    x = O.synth_read(77, 100_000)
+    fr = _frames(x)
+    out = {}
+    # the M frame claims 2^20 bytes more than it holds
+    f = list(fr)
+    cs_m = len(O.c5_streams(x)[2])
+    f[2] = _set_fcs(fr[2], cs_m + (1 << 20))
+    out["m_claims_1MiB_more"] = (O.c5_assemble(f), x.size)
+    # the keys frame claims 2^41 bytes: the sum passes 2^40
+    f = list(fr)
+    f[0] = _set_fcs(fr[0], 1 << 41)
+    out["keys_claims_2TiB"] = (O.c5_assemble(f), x.size)
+    # the Lhigh frame really holds 300,000 zero bytes (RLE blocks): the reference decodes it
+    f = list(fr)
+    f[4] = O.zstd_compress1(np.zeros(300_000, np.uint8))
+    out["lhigh_expands_300k"] = (O.c5_assemble(f), x.size)
+    return x, out
+
+
+def _decode_batch(codec, blobs, lens):
+    import torch
+
+    dev = torch.device("cuda", 0)
+    sizes = np.array([len(b) for b in blobs], np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    flat = np.frombuffer(b"".join(blobs), np.uint8).copy()
+    counts = np.asarray(lens, np.int32)
+    out, _, st = codec.decompress_batch(torch.from_numpy(flat).to(dev), torch.from_numpy(offs).to(dev),
+                                        torch.from_numpy(sizes).to(dev), torch.from_numpy(counts).to(dev))
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), st.cpu().numpy()
+
+
+EXPECT_GPU = {"m_claims_1MiB_more": 3, "keys_claims_2TiB": 8, "lhigh_expands_300k": 9}
+
+
+@pytest.fixture(scope="module")
+def codecs():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from rawnanoporesignalcompression_amd import PGNanoCodec
+
+    plain = PGNanoCodec(0)
+    keys = ("PGN_DEFER_MIN_CHUNKS", "PGN_DEFER_G")
+    old = {k: os.environ.get(k) for k in keys}
+    os.environ["PGN_DEFER_MIN_CHUNKS"] = "1"
+    os.environ["PGN_DEFER_G"] = "96"
+    try:
+        deferred = PGNanoCodec(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    yield plain, deferred
+    plain.close()
+    deferred.close()
+
+
+def test_oracle_statuses():
+    """CPU: the oracle (libzstd) reaches the reference's statuses on the crafted blobs."""
+    _, cases = _cases()
+    got = {k: O.c5_decompress(b, n)[0] for k, (b, n) in cases.items()}
+    assert got == {"m_claims_1MiB_more": 3, "keys_claims_2TiB": 8, "lhigh_expands_300k": 4}
+
+
+@pytest.mark.gpu
+def test_over_claim_statuses_per_chunk(codecs):
+    from rawnanoporesignalcompression_amd import PGNanoError
+
+    plain, _ = codecs
+    _, cases = _cases()
+    for k, (b, n) in cases.items():
+        with pytest.raises(PGNanoError) as ei:
+            plain.decompress_signal(b, sample_count=n)
+        assert ei.value.status == EXPECT_GPU[k], k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", [0, 1])
+def test_over_claim_statuses_in_batches(codecs, which):
+    """Between valid chunks: a 130-chunk batch (staged passes; with the deferred codec, the deferred
+    Huffman sections); the valid chunks decode, the corrupted ones get their statuses."""
+    codec = codecs[which]
+    x, cases = _cases()
+    ok_blob = O.c5_compress(x)[1]
+    names = list(cases)
+    blobs, lens, want = [], [], []
+    for i in range(130):
+        if i % 10 == 3:
+            k = names[(i // 10) % len(names)]
+            blobs.append(cases[k][0])
+            want.append(EXPECT_GPU[k])
+        else:
+            blobs.append(ok_blob)
+            want.append(0)
+        lens.append(x.size)
+    out, st = _decode_batch(codec, blobs, lens)
+    assert st.tolist() == want
+    for i in range(130):
+        if want[i] == 0:
+            assert np.array_equal(out[i * x.size:(i + 1) * x.size], x), i

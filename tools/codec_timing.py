@@ -20,5 +20,5 @@ for _ in range(K + 1):
     e.append(c.last_encode_ms())
     d.append(c.last_decode_ms())
 ok = bool(torch.equal(out, samples))
-e, d = sorted(e[1:]), sorted(d[1:])
+e, d = (sorted(e[1:]), sorted(d[1:])) if K > 0 else (e, d)
 print(f"R={R} encode ms min {e[0]:.3f} med {e[len(e)//2]:.3f}  decode ms min {d[0]:.3f} med {d[len(d)//2]:.3f}  ok {ok}")

@@ -27,8 +27,8 @@ else:
     out, so, st = c.decompress_batch(enc.blobs, enc.offsets, enc.sizes, cnt)
     torch.cuda.synchronize()
     print("encode ms", c.last_encode_ms(), "decode ms", c.last_decode_ms(), "ok", bool(torch.equal(out, samples)))
-buf = np.zeros(64, np.uint64)
-c._lib.pgn_debug_phase_cycles(c._h, buf.ctypes.data, 64)
+buf = np.zeros(128, np.uint64)
+c._lib.pgn_debug_phase_cycles(c._h, buf.ctypes.data, 128)
 for name, lab, arr in (("encode", ENC, buf[:16]), ("decode", DEC, buf[16:])):
     tot = float(arr.sum())
     print(f"{name}: total {tot/1e9:.2f} Gcycles (summed over waves), per chunk {tot/R/1e3:.1f} kcycles")
@@ -50,3 +50,16 @@ print("encode counters per chunk:")
 for i, l in enumerate(ECNT):
     if buf[32 + i]:
         print(f"   {l:24s} {buf[32 + i] / R:12.2f}")
+
+HUF = ["tables (job flags, compact tables to LDS)", "setup + 8-iteration prologue", "trips of 8 iterations",
+       "drain, head/tail bytes, last symbols, end check"]
+hp, hc = buf[64:80], buf[96:112]
+tot = float(hp.sum())
+if tot:
+    print(f"dec_huf_kernel: total {tot/1e9:.2f} Gcycles (summed over waves), per chunk {tot/R/1e3:.1f} kcycles")
+    for i, l in enumerate(HUF):
+        print(f"   {l:48s} {100*hp[i]/tot:6.2f}%  {hp[i]/R/1e3:9.1f} kcyc/chunk")
+    waves = max(int(hc[0]), 1)
+    print(f"   waves {waves}, trips per wave {hc[1]/waves:.1f}, live lanes per wave {hc[2]/waves:.1f}, "
+          f"symbols per chunk {hc[3]/R:.0f}, wave-cycles per wave {tot/waves/1e3:.1f} k, "
+          f"per trip {hp[2]/max(hc[1],1):.0f}")
