@@ -544,20 +544,35 @@ __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, uint3
     }
 }
 
-// One step's bookkeeping, computed a step ahead: the key word, the class counts below this lane,
-// the step's totals and the staging ranges of its S / M / class-3 bytes.
-struct MergePlan {
+// One step's bookkeeping, computed two steps ahead: the key word, the class counts below this lane,
+// the step's totals, the staging ranges of its S / M / class-3 bytes, and the stream counts before it.
+struct MergePlan {  // offsets in the intermediate are 32-bit (a chunk's intermediate is < 40 MB)
     uint32_t kw;
     uint32_t excl;        // classes 1 | 2 << 11 | 3 << 22 of the lanes below (exact: at most 1008 each)
     uint32_t ns, nm, nl;  // the step's class counts
-    uint64_t aS, aS0, aM, aM0;
-    uint32_t nwS, nbM;  // S dwords, M 16-byte blocks from aS0 / aM0
+    uint32_t sN, mN, lN;  // S nibbles / M bytes / class-3 pairs before the step
+    uint32_t nwS, nbM;    // S dwords, M 16-byte blocks from the 16-byte blocks holding the step's first bytes
+};
+// A step's stream bytes in flight (loaded two steps before they are staged)
+struct MergeBytes {
+    uint4 vM;
+    uint32_t vS, lb, hb;
 };
 
 // The merge of the steps [t0, t1) of a chunk (t0 a multiple of kSplitStep, t1 = n or one), given
 // the class counts of the samples before t0 (sN0 / mN0 / lN0) and the running sum there (carry, in
 // and out); *lEnd receives the class-3 count through t1.  c5_merge_wave is the whole chunk in one
 // call; dec_merge_lb_kernel gives the ranges of one chunk to single-wave workgroups.
+// Software pipeline (one wave per chunk): a step's key word is loaded kMergeAhead + 2 steps ahead,
+// its plan made and its S / M / class-3 bytes loaded kMergeAhead steps ahead (kMergeAhead = 2: two
+// register sets, the loop unrolled by two).  Measured (tools/gpu_ab_kern.sh, 20,000 chunks): two
+// steps ahead is no faster than one (1.54 vs 1.50 ms; the merge is issue-bound), and at
+// six waves per SIMD it spills; so one.  Plan offsets are 32-bit (fewer scalar instructions).
+#ifndef PGN_MERGE_AHEAD
+#define PGN_MERGE_AHEAD 1
+#endif
+constexpr uint32_t kMergeAhead = PGN_MERGE_AHEAD;
+static_assert(kMergeAhead == 1 || kMergeAhead == 2, "merge lookahead");
 template <bool C4 = false>
 __device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, uint64_t total, uint64_t dS, uint64_t dM,
                                               uint64_t dLl, int16_t* __restrict__ out, uint32_t n, uint32_t t0,
@@ -566,9 +581,13 @@ __device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, ui
 {
     using CO = ClassOffsets<C4>;
     const uint32_t lane = (uint32_t)lane_id();
-    const uint64_t kl = ((uint64_t)n + 3) / 4;
-    const uint64_t ps = kl, pm = kl + dS, pl = kl + dS + dM, ph = kl + dS + dM + dLl;
-    uint64_t sN = sN0, mN = mN0, lN = lN0;  // nibbles / bytes consumed so far (wave-uniform)
+    // stream starts, 32-bit: an intermediate is below 2^31 bytes (inter_cap), the key bytes below
+    // 2^22 and the decoded sizes sum to at most `total`, so no sum below overflows
+    if (total >= 0x80000000ull || dS + dM + dLl > total) return 1;
+    const uint32_t tot = (uint32_t)total;
+    const uint32_t kl = (n + 3) / 4;
+    const uint32_t ps = kl, pm = kl + (uint32_t)dS, pl = pm + (uint32_t)dM, ph = pl + (uint32_t)dLl;
+    uint32_t sN = (uint32_t)sN0, mN = (uint32_t)mN0, lN = (uint32_t)lN0;  // before the next step to plan (wave-uniform)
     if (lane == 0) W.zero[0] = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {  // the S table: byte -> two entries
@@ -580,7 +599,7 @@ __device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, ui
     auto key_word = [&](uint32_t t) -> uint32_t {
         const bool full = t + kSplitStep <= n;
         const uint32_t nK = full ? kSplitStep / 4 : (n - t + 3) / 4;
-        const uint64_t kb0 = t >> 2;
+        const uint32_t kb0 = t >> 2;
         uint32_t kw = 0;
         if (4u * lane + 4u <= nK) {
             kw = ld32u(in + kb0 + 4u * lane);
@@ -593,10 +612,11 @@ __device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, ui
         }
         return kw;
     };
-    // the plan of step t from its key word; false if the step reads past `total` (the reference's UB)
+    // the plan of step t from its key word (the counts advance past it); false if the step reads
+    // past `total` (the reference's UB)
     auto plan = [&](uint32_t t, uint32_t kw, MergePlan& pn) -> bool {
         const uint32_t nK = t + kSplitStep <= n ? kSplitStep / 4 : (n - t + 3) / 4;
-        if ((t >> 2) + nK > total) return false;
+        if ((t >> 2) + nK > tot) return false;
         const uint32_t lo = kw & 0x55555555u, hi = (kw >> 1) & 0x55555555u;
         const uint32_t pc = (uint32_t)__builtin_popcount(lo & ~hi) | ((uint32_t)__builtin_popcount(hi & ~lo) << 11) |
                             ((uint32_t)__builtin_popcount(lo & hi) << 22);
@@ -609,77 +629,99 @@ __device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, ui
         pn.ns = t12 & 0x7FFu;
         pn.nm = (t12 >> 11) & 0x7FFu;
         pn.nl = (e63 >> 22) + (p63 >> 22);
-        if (ps + ((sN + pn.ns + 1) >> 1) > total || pm + mN + pn.nm > total || pl + lN + pn.nl > total ||
-            ph + lN + pn.nl > total)
+        if (ps + ((sN + pn.ns + 1) >> 1) > tot || pm + mN + pn.nm > tot || pl + lN + pn.nl > tot || ph + lN + pn.nl > tot)
             return false;
-        pn.aS = ps + (sN >> 1);
-        pn.aS0 = pn.aS & ~(uint64_t)15;
-        pn.nwS = (uint32_t)((ps + ((sN + pn.ns + 1) >> 1) - pn.aS0 + 3) >> 2);
-        pn.aM = pm + mN;
-        pn.aM0 = pn.aM & ~(uint64_t)15;
-        pn.nbM = (uint32_t)((pn.aM + pn.nm - pn.aM0 + 15) >> 4);
+        const uint32_t aS = ps + (sN >> 1), aM = pm + mN;
+        pn.nwS = ((ps + ((sN + pn.ns + 1) >> 1)) - (aS & ~15u) + 3) >> 2;
+        pn.nbM = (aM + pn.nm - (aM & ~15u) + 15) >> 4;
+        pn.sN = sN;
+        pn.mN = mN;
+        pn.lN = lN;
+        sN += pn.ns;
+        mN += pn.nm;
+        lN += pn.nl;
         return true;
+    };
+    auto load_stage = [&](const MergePlan& pn, MergeBytes& B) {
+        const uint32_t aS0 = (ps + (pn.sN >> 1)) & ~15u, aM0 = (pm + pn.mN) & ~15u;
+        if (lane < pn.nwS) B.vS = gld<uint32_t>(in + aS0 + 4u * lane);
+        if (lane < pn.nbM) B.vM = gld<uint4>(in + aM0 + 16u * lane);
+        if (lane < pn.nl) {
+            B.lb = gb(in + pl + pn.lN + lane);
+            B.hb = gb(in + ph + pn.lN + lane);
+        }
     };
     if (t0 >= t1) {
         *lEnd = lN;
         return 0;
     }
-    // prologue: step t0's plan and staged bytes, step t0 + 1's key word
-    MergePlan cur;
-    if (!plan(t0, key_word(t0), cur)) return 1;
-    uint32_t kwNext = t0 + kSplitStep < t1 ? key_word(t0 + kSplitStep) : 0u;
-    uint4 vM = make_uint4(0, 0, 0, 0);
-    uint32_t vS = 0, lb = 0, hb = 0;
-    auto load_stage = [&](const MergePlan& pn) {
-        if (lane < pn.nwS) vS = gld<uint32_t>(in + pn.aS0 + 4u * lane);
-        if (lane < pn.nbM) vM = gld<uint4>(in + pn.aM0 + 16u * lane);
-        if (lane < pn.nl) {
-            lb = gb(in + pl + lN + lane);
-            hb = gb(in + ph + lN + lane);
-        }
-    };
-    load_stage(cur);
+    const uint32_t nsteps = (t1 - t0 + kSplitStep - 1) / kSplitStep;
+    auto tof = [&](uint32_t j) { return t0 + j * kSplitStep; };
+    // prologue: the plans and bytes of steps 0 .. kMergeAhead - 1, the key words of the next two
+    constexpr uint32_t D = kMergeAhead;
+    MergePlan P0, P1;
+    MergeBytes B0, B1;
+    B0.vM = B1.vM = make_uint4(0, 0, 0, 0);
+    B0.vS = B1.vS = B0.lb = B1.lb = B0.hb = B1.hb = 0;
+    if (!plan(tof(0), key_word(tof(0)), P0)) return 1;
+    load_stage(P0, B0);
+    if (D == 2 && nsteps > 1) {
+        if (!plan(tof(1), key_word(tof(1)), P1)) return 1;
+        load_stage(P1, B1);
+    }
+    uint32_t kwN1 = nsteps > D ? key_word(tof(D)) : 0u;          // the next plan's key word
+    uint32_t kwN2 = nsteps > D + 1 ? key_word(tof(D + 1)) : 0u;  // and the one after it
     lds_sync();
-    for (uint32_t t = t0; t < t1; t += kSplitStep) {
+    // step j from plan P / bytes B; then plan step j + D into P and load its bytes into B
+    auto body = [&](uint32_t j, MergePlan& P, MergeBytes& B) -> bool {
+        const uint32_t t = tof(j);
         const bool full = t + kSplitStep <= n;
-        // ---- this step's bytes into the window (loaded a step ago): S by table, M and class 3 by arithmetic
+        // ---- this step's bytes into the window: S by table, M and class 3 by arithmetic
         // S: four bytes (eight entries) per lane, so the step's ~170 S bytes take four table reads
         // per lane instead of sixteen on a quarter of the lanes
-        const uint32_t eM = 8u * cur.nwS, eL = eM + 16u * cur.nbM;
+        const uint32_t eM = 8u * P.nwS, eL = eM + 16u * P.nbM;
+        const uint32_t aS = ps + (P.sN >> 1), aM = pm + P.mN, aS0 = aS & ~15u, aM0 = aM & ~15u;
         {
             constexpr uint32_t add2 = CO::o2 * 0x00010001u;
             auto put_s4 = [&](uint32_t b, uint32_t v) {
                 *(uint4*)(W.V + 8u * b) = make_uint4(W.nib[v & 0xFFu], W.nib[(v >> 8) & 0xFFu], W.nib[(v >> 16) & 0xFFu],
                                                      W.nib[v >> 24]);
             };
-            if (lane < cur.nwS) put_s4(lane, vS);
-            if (lane < cur.nbM) put_bytes16(W.V + eM + 16u * lane, vM, add2);
-            if (lane < cur.nl) W.V[eL + lane] = zz_dec16((uint16_t)((lb | (hb << 8)) + CO::o3));
-            for (uint32_t b = lane + 64; b < cur.nwS; b += 64) put_s4(b, gld<uint32_t>(in + cur.aS0 + 4u * b));
-            for (uint32_t b = lane + 64; b < cur.nbM; b += 64) put_bytes16(W.V + eM + 16u * b, gld<uint4>(in + cur.aM0 + 16u * b), add2);
-            for (uint32_t i = lane + 64; i < cur.nl; i += 64)
-                W.V[eL + i] = zz_dec16((uint16_t)(((uint32_t)gb(in + pl + lN + i) | ((uint32_t)gb(in + ph + lN + i) << 8)) + CO::o3));
+            if (lane < P.nwS) put_s4(lane, B.vS);
+            if (lane < P.nbM) put_bytes16(W.V + eM + 16u * lane, B.vM, add2);
+            if (lane < P.nl) W.V[eL + lane] = zz_dec16((uint16_t)((B.lb | (B.hb << 8)) + CO::o3));
+            for (uint32_t b = lane + 64; b < P.nwS; b += 64) put_s4(b, gld<uint32_t>(in + aS0 + 4u * b));
+            for (uint32_t b = lane + 64; b < P.nbM; b += 64) put_bytes16(W.V + eM + 16u * b, gld<uint4>(in + aM0 + 16u * b), add2);
+            for (uint32_t i = lane + 64; i < P.nl; i += 64)
+                W.V[eL + i] = zz_dec16((uint16_t)(((uint32_t)gb(in + pl + P.lN + i) | ((uint32_t)gb(in + ph + P.lN + i) << 8)) + CO::o3));
         }
         lds_sync();
         // LDS byte places of my first value of each class
         constexpr uint32_t offV = (uint32_t)__builtin_offsetof(MergeLds, V);
-        const uint32_t pS = offV + 2u * ((uint32_t)(2 * (cur.aS - cur.aS0) + (sN & 1)) + (cur.excl & 0x7FFu));
-        const uint32_t pM = offV + 2u * (eM + (uint32_t)(cur.aM - cur.aM0) + ((cur.excl >> 11) & 0x7FFu));
-        const uint32_t pL = offV + 2u * (eL + (cur.excl >> 22));
-        const uint32_t kw = cur.kw;
-        sN += cur.ns;
-        mN += cur.nm;
-        lN += cur.nl;
-        // ---- the next step: its plan (key word loaded a step ago), its bytes in flight during this merge
-        const uint32_t tn = t + kSplitStep;
-        bool more = tn < t1;
-        if (more) {
-            if (!plan(tn, kwNext, cur)) return 1;
-            if (tn + kSplitStep < t1) kwNext = key_word(tn + kSplitStep);
-            load_stage(cur);
+        const uint32_t pS = offV + 2u * ((2 * (aS - aS0) + (P.sN & 1u)) + (P.excl & 0x7FFu));
+        const uint32_t pM = offV + 2u * (eM + (aM - aM0) + ((P.excl >> 11) & 0x7FFu));
+        const uint32_t pL = offV + 2u * (eL + (P.excl >> 22));
+        const uint32_t kw = P.kw;
+        // ---- step j + D: its plan (key word loaded two steps ago), its bytes in flight for D steps
+        if (j + D < nsteps) {
+            if (!plan(tof(j + D), kwN1, P)) return false;
+            load_stage(P, B);
         }
+        kwN1 = kwN2;
+        if (j + D + 2 < nsteps) kwN2 = key_word(tof(j + D + 2));
         merge_step(W, kw, pS, pM, pL, carry, out, t, n, full);
         lds_sync();
+        return true;
+    };
+    if (D == 1) {
+        for (uint32_t j = 0; j < nsteps; j++)
+            if (!body(j, P0, B0)) return 1;
+    } else {
+        for (uint32_t j = 0; j < nsteps; j += 2) {
+            if (!body(j, P0, B0)) return 1;
+            if (j + 1 >= nsteps) break;
+            if (!body(j + 1, P1, B1)) return 1;
+        }
     }
     *lEnd = lN;
     return 0;

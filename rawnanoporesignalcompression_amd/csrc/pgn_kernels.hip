@@ -122,8 +122,10 @@ __host__ __device__ constexpr size_t inter_cap(uint32_t capN) { return (size_t)c
 constexpr size_t kVbzPadding = 16;
 constexpr uint64_t kAllocLimit = (uint64_t)1 << 40;  // a decode intermediate above this is an allocation failure (PGN_ERR_ALLOC)
 __host__ __device__ constexpr size_t chunk_inter_bytes(uint32_t capN) { return align_up(inter_cap(capN) + 64, 256); }
-// per-chunk decode buffers of the two passes in flight (intermediates, records, Huffman jobs)
-constexpr size_t kDecBufferBudget = (size_t)24 << 30;
+// per-chunk decode buffers of the passes in flight (intermediates, records, Huffman jobs), all
+// buffers together
+constexpr size_t kDecBufferBudget = (size_t)32 << 30;
+constexpr int kMaxDecBufs = 4;  // decode pass buffers in rotation (pgn_ctx::decBufs)
 
 // Work-unit order of the per-stream kernels: the large streams first (M, S, keys, Llow, Lhigh), so
 // the dynamic queue ends with short units.
@@ -602,7 +604,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void de
         // (the record's fields are read again for the call: kept live across the fast path they
         // pushed this kernel from 37 to 186 spilled VGPRs)
         P.mark(3);
-        long r = dec_frame_fast(a.in + d.src, d.len, dst, cap, S.job, S.htab, P);
+        long r = dec_frame_fast(a.in + d.src, d.len, dst, cap, S.job, S.htab, P, sDec.hb);
         P.mark(2);  // (phase 2: the fast path, or its fall-through)
         if (r < 0) r = zstd_decompress_wave(a.in + d.src, d.len, dst, cap, S, P);
         if (lane == 0) d.dres = (int32_t)r;
@@ -1750,7 +1752,7 @@ struct pgn_ctx {
     // dec_huf_kernel (pgn_hufjob.h), in passes of up to deferG chunks: a lane-per-stream decoder
     // needs thousands of frames in flight (PGN_DEFER_MIN_CHUNKS / PGN_DEFER_G tune both; the output
     // is the same either way)
-    size_t deferMin = 12288, deferG = 32768;
+    size_t deferMin = 12288, deferG = 12500;
     bool lastDeferred = false;  // the last staged C5 decode deferred its Huffman sections (pgn_ctx_kernels)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
@@ -1787,6 +1789,13 @@ struct pgn_ctx {
     // can share the CUs with the Huffman sections of pass p + 1 (latency-bound)
     hipStream_t mergeS = nullptr;
     hipEvent_t evHuf[2] = {nullptr, nullptr};
+    // decode passes: buffers in rotation (PGN_DEC_BUFS, 2..kMaxDecBufs) with their stage / sections /
+    // free events, and the streams the deferred sections alternate over (PGN_HUF_STREAMS, 1 or 2)
+    // measured (tools/gpu_env_sweep.sh, 100,000 chunks): 2 buffers / 1 stream / passes of 20,000:
+    // decode 23.1 ms; 4 / 2 / 12,500: 22.7 ms (profiles/r05_decode_pipeline_sweep.log)
+    size_t decBufs = 4, hufStreams = 2;
+    hipStream_t side2 = nullptr;
+    hipEvent_t evDStage[kMaxDecBufs] = {}, evDHuf[kMaxDecBufs] = {}, evDFree[kMaxDecBufs] = {};
     uint64_t* prof = nullptr;  // kProfWords: phase cycles and counters (encode, decode, dec_huf) when PGN_PHASE_PROFILE=1
     bool encTimed = false, decTimed = false;
     // Stream ordering of the context's shared state (work counters, slot scratch, per-chunk buffers):
@@ -1916,6 +1925,17 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     HIPCHK(hipEventCreateWithFlags(&c->evLast, hipEventDisableTiming));
     HIPCHK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->mergeS, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking));
+    for (int i = 0; i < kMaxDecBufs; i++) {
+        HIPCHK(hipEventCreateWithFlags(&c->evDStage[i], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->evDHuf[i], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&c->evDFree[i], hipEventDisableTiming));
+    }
+    if (const char* v = getenv("PGN_DEC_BUFS")) {
+        const long x = atol(v);
+        if (x >= 2 && x <= kMaxDecBufs) c->decBufs = (size_t)x;
+    }
+    if (const char* v = getenv("PGN_HUF_STREAMS")) c->hufStreams = atol(v) == 2 ? 2 : 1;
     HIPCHK(hipStreamCreateWithFlags(&c->scanStream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->evScanFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->evScan, hipEventDisableTiming));
@@ -1967,12 +1987,17 @@ int pgn_ctx_destroy(pgn_ctx* c)
     for (int i = 0; i < 4; i++) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->mergeS) (void)hipStreamSynchronize(c->mergeS);
+    if (c->side2) (void)hipStreamSynchronize(c->side2);
+    for (int i = 0; i < kMaxDecBufs; i++)
+        for (hipEvent_t e : {c->evDStage[i], c->evDHuf[i], c->evDFree[i]})
+            if (e) (void)hipEventDestroy(e);
     if (c->evLast) (void)hipEventSynchronize(c->evLast);
     for (hipEvent_t e : {c->evFork, c->evJoin, c->evStage[0], c->evStage[1], c->evFree[0], c->evFree[1], c->evLast, c->evHuf[0],
                          c->evHuf[1]})
         if (e) (void)hipEventDestroy(e);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->mergeS) (void)hipStreamDestroy(c->mergeS);
+    if (c->side2) (void)hipStreamDestroy(c->side2);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return PGN_OK;
@@ -2281,8 +2306,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     bool defer = codec == kCodecC5 && nchunks >= c->deferMin;
     const size_t stride = chunk_inter_bytes(capCall);
     size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
-    if (defer) {  // up to deferG chunks per pass, and two passes' buffers within kDecBufferBudget
-        size_t gmax = kDecBufferBudget / (2 * (stride + kStreams * (sizeof(DecUnit) + kJobBytes)));
+    if (defer) {  // up to deferG chunks per pass, and decBufs passes' buffers within kDecBufferBudget
+        size_t gmax = kDecBufferBudget / (c->decBufs * (stride + kStreams * (sizeof(DecUnit) + kJobBytes)));
         gmax = gmax < c->deferG ? gmax : c->deferG;
         gmax = gmax < c->subBatch ? c->subBatch : gmax;
         const size_t np = (nchunks + gmax - 1) / gmax;
@@ -2294,7 +2319,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots;  // few chunks: a workgroup per frame
     defer = defer && !coop;  // the cooperative kernel decodes its sections itself
     c->lastDeferred = defer;
-    const size_t nbuf = passes > 1 ? 2 : 1;
+    // buffers in rotation: a pass parses into buffer p % nbuf once the merge of pass p - nbuf has read it
+    const size_t nbuf = passes > 1 ? (passes < c->decBufs ? passes : c->decBufs) : 1;
     const size_t unitBytes = align_up(G * kStreams * sizeof(DecUnit), 256);
     const size_t bufBytes = G * stride + unitBytes + (defer ? G * kStreams * kJobBytes + kHufJunkBytes : 0);
     int rc = ensure_dec(c, slots, nbuf * bufBytes);
@@ -2306,9 +2332,15 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     // stays on the caller's stream
 #ifdef PGN_SERIAL_DECODE  // diagnostic builds: every decode kernel on the caller's stream (isolated kernel times)
     const hipStream_t sideS = s;
+    const bool multi = false;
 #else
     const hipStream_t sideS = passes > 1 ? c->side : s;
+    const bool multi = passes > 1;
 #endif
+    // deferred sections over several passes: the sections of pass p on hufS[p % hufStreams], the merges
+    // on a third stream behind them
+    const hipStream_t hufS[2] = {c->side, c->side2};
+    const size_t hufStreams = c->hufStreams;
     if (passes > 1) {
         HIPCHK(hipEventRecord(c->evFork, s));
         HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
@@ -2336,11 +2368,10 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         const int lrc = take_lookback(c, s, a.lookback, a.epoch);
         if (lrc) return lrc;
     }
-    // pass p: parse + zstd on the caller's stream into buffer p % 2, the deferred Huffman sections and
-    // the merge on the side stream.  Those of pass p overlap the zstd kernel of pass p+1; a buffer is
-    // parsed into again only after the merge of the pass before last has read it.
+    // pass p: parse + zstd on the caller's stream into buffer p % nbuf, the deferred Huffman sections
+    // and the merge on the side streams.  Those of pass p overlap the zstd kernel of pass p+1.
     for (size_t p = 0; p < passes; p++) {
-        const int b = (int)(p & 1);
+        const int b = (int)(p % nbuf);
         uint8_t* buf = c->decChunks + (size_t)b * bufBytes;
         a.inter = buf;
         a.units = (DecUnit*)(buf + G * stride);
@@ -2349,45 +2380,40 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         c->lastG = G;
         a.base = p * G;
         a.queue = c->qCur + p;
-        if (p >= 2) HIPCHK(hipStreamWaitEvent(s, c->evFree[b], 0));
+        if (p >= nbuf) HIPCHK(hipStreamWaitEvent(s, c->evDFree[b], 0));
         a.coopParse = (coop && codec != kCodecVbz) ? 1u : 0u;
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         else if (!a.coopParse) hipLaunchKernelGGL(dec_parse_kernel, dim3((unsigned)((G + 63) / 64)), dim3(64), 0, s, a);
         if (coop)
             hipLaunchKernelGGL(dec_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopWaves), 0, s, a);
         else hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
-#ifdef PGN_K2_MAIN  // A/B builds: the deferred sections on the caller's stream, before the next pass's frames
-        if (defer)
-            hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, s, a);
-#endif
-        if (passes > 1) {
-            HIPCHK(hipEventRecord(c->evStage[b], s));
-            HIPCHK(hipStreamWaitEvent(c->side, c->evStage[b], 0));
+        // the stream of this pass's sections (deferred) or merge (otherwise)
+        const hipStream_t hs = multi ? (defer ? hufS[p % hufStreams] : c->side) : sideS;
+        if (multi) {
+            HIPCHK(hipEventRecord(c->evDStage[b], s));
+            HIPCHK(hipStreamWaitEvent(hs, c->evDStage[b], 0));
         }
-#ifndef PGN_K2_MAIN
-        // the deferred sections (kHufFrames frames of one stream type per wave) on the side stream,
-        // ahead of the pass's merge: they overlap the next pass's frame decode (LDS- and
-        // latency-bound beside a scalar- and latency-bound kernel)
+        // the deferred sections (kHufFrames frames of one stream type per wave), ahead of the pass's
+        // merge: they overlap the next pass's frame decode
         if (defer)
-            hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, sideS, a);
-#endif
+            hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, hs, a);
         // with deferred sections over several passes the merge goes to the third stream behind its
         // pass's sections (so it overlaps the next pass's sections); the buffer is free after it
-        hipStream_t ms = sideS;
-        if (defer && passes > 1) {
-            HIPCHK(hipEventRecord(c->evHuf[b], c->side));
-            HIPCHK(hipStreamWaitEvent(c->mergeS, c->evHuf[b], 0));
+        hipStream_t ms = hs;
+        if (defer && multi) {
+            HIPCHK(hipEventRecord(c->evDHuf[b], hs));
+            HIPCHK(hipStreamWaitEvent(c->mergeS, c->evDHuf[b], 0));
             ms = c->mergeS;
         }
         if (codec == kCodecVbz) hipLaunchKernelGGL(vbz_merge_kernel, dim3((unsigned)G), dim3(64), 0, ms, a);
         else if (a.lookback)  // few chunks: kMergeRanges single-wave workgroups per chunk
             hipLaunchKernelGGL(dec_merge_lb_kernel, dim3((unsigned)(G * kMergeRanges)), dim3(64), 0, ms, a);
         else hipLaunchKernelGGL(dec_merge_kernel, dim3((unsigned)G), dim3(64), 0, ms, a);
-        if (passes > 1) HIPCHK(hipEventRecord(c->evFree[b], ms));
+        if (passes > 1) HIPCHK(hipEventRecord(c->evDFree[b], ms));
     }
     HIPCHK(hipGetLastError());
-    if (passes > 1) {  // the last merge follows every other launch of the call on the side streams
-        HIPCHK(hipEventRecord(c->evJoin, (defer && passes > 1) ? c->mergeS : c->side));
+    if (multi) {  // the last merge follows every other launch of the call on the side streams
+        HIPCHK(hipEventRecord(c->evJoin, defer ? c->mergeS : c->side));
         HIPCHK(hipStreamWaitEvent(s, c->evJoin, 0));
     }
     return PGN_OK;

@@ -23,6 +23,16 @@ constexpr uint32_t kJobTabUse = 504;  // entries a table may have: dec_huf_kerne
 constexpr unsigned kHufLdsLog = 11;  // Huffman tables up to this log live in LDS (zstd's encoders
                                      // never exceed 11); a 12-bit table is built in HBM (slow path)
 
+// The Huffman table build's LDS (huf_build_dtable_body): part of DecLds in the frame decoder, a
+// __shared__ of its own (1 KiB) in dec_zfast_kernel, which builds only jobs' compact tables.
+struct HufBuildLds {
+    uint8_t wts[256];         // weights of the current table
+    uint8_t order[256];       // symbols sorted by (weight, symbol)
+    uint8_t hbuf[272];        // staged Huffman table description (zero padded)
+    z1::FseDEntry wdt[64];    // weights FSE decode table (tableLog <= 6)
+    int16_t wnorm[16];
+};
+
 // Per-workgroup LDS, sized for four decode waves per SIMD: the literal stage (table, boundary
 // bitmap, staging rows) and the sequences stage overlay each other.  A Huffman table that must
 // outlive a sequences stage (treeless literals in a later block) is parked in HBM (DecScratch::htab).
@@ -33,13 +43,7 @@ struct alignas(16) DecLds {
             union {
                 // per-lane arrays are word-major ([word][lane]): lanes touching their own rows hit distinct banks
                 uint32_t stg[kStgWords][64];  // staged stream bytes of the current round
-                struct {                      // table build only (done before the rounds start)
-                    uint8_t wts[256];         // weights of the current table
-                    uint8_t order[256];       // symbols sorted by (weight, symbol)
-                    uint8_t hbuf[272];        // staged Huffman table description (zero padded)
-                    z1::FseDEntry wdt[64];    // weights FSE decode table (tableLog <= 6)
-                    int16_t wnorm[16];
-                };
+                HufBuildLds hb;               // table build only (done before the rounds start)
             };
         };
         struct {  // sequences stage
@@ -290,7 +294,7 @@ __device__ __forceinline__ size_t ncount_lds(int16_t* norm, unsigned* maxSVPtr, 
 // valid position to the symbol whose cumulative positive count covers k: lane u computes its
 // position, its rank among the valid ones (ballot + mbcnt) and that symbol directly.  The state
 // of entry u counts the earlier entries of its symbol (one ballot per symbol).
-__device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxSV, unsigned tableLog)
+__device__ __forceinline__ bool wdtable_build(HufBuildLds& H, const int16_t* norm, unsigned maxSV, unsigned tableLog)
 {
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t tableSize = 1u << tableLog;
@@ -302,15 +306,15 @@ __device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxS
     const uint32_t nLow = readlane_u32(lowIncl, 63), total = readlane_u32(cntIncl, 63);
     const uint32_t highThreshold = tableSize - 1 - nLow;
     if (total != highThreshold + 1) return false;  // the serial spread's final `position != 0`
-    if (low) sDec.wdt[tableSize - lowIncl].symbol = (uint8_t)lane;
+    if (low) H.wdt[tableSize - lowIncl].symbol = (uint8_t)lane;
     const uint32_t q = (lane * step) & mask;
     const bool valid = lane < tableSize && q <= highThreshold;
     const uint32_t k = mbcnt(ballot(valid));
     uint32_t sym = 0;  // number of symbols whose cumulative count is <= k
     for (unsigned sy = 0; sy <= maxSV; sy++) sym += readlane_u32(cntIncl, (int)sy) <= k ? 1u : 0u;
-    if (valid) sDec.wdt[q].symbol = (uint8_t)sym;
+    if (valid) H.wdt[q].symbol = (uint8_t)sym;
     lds_sync();
-    const uint32_t su = lane < tableSize ? sDec.wdt[lane].symbol : 0xFFu;
+    const uint32_t su = lane < tableSize ? H.wdt[lane].symbol : 0xFFu;
     uint32_t rank = 0;
     for (unsigned sy = 0; sy <= maxSV; sy++) {
         const uint64_t m = ballot(su == sy);
@@ -321,18 +325,20 @@ __device__ __forceinline__ bool wdtable_build(const int16_t* norm, unsigned maxS
     if (lane < tableSize) {
         const uint32_t nextState = start + rank;
         const uint32_t nb = tableLog - z1::highbit32(nextState);
-        sDec.wdt[lane].nbBits = (uint8_t)nb;
-        sDec.wdt[lane].newState = (uint16_t)((nextState << nb) - tableSize);
+        H.wdt[lane].nbBits = (uint8_t)nb;
+        H.wdt[lane].newState = (uint16_t)((nextState << nb) - tableSize);
     }
     lds_sync();
     return true;
 }
 
 // Returns header bytes consumed (0 = corrupt); *tlOut = table log, *minNbOut = its shortest code.
-// Fills sDec.tab, or gt (4096 entries in HBM) for a 12-bit table.
+// Fills sDec.tab, or gt (4096 entries in HBM) for a 12-bit table; JobOnly (dec_frame_fast): only the
+// job's compact table, so the kernel needs no more LDS than H.
 // hw: when not null, the frame's header window (loaded at frame offset 0) and src at frame offset hoff:
 // the description is staged from it (lane-permute reads, no memory round trip) when it lies inside
-__device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
+template <bool JobOnly = false>
+__device__ __forceinline__ size_t huf_build_dtable_body(HufBuildLds& H, const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
                                                        unsigned* minNbOut, const HdrWin* hw = nullptr, uint32_t hoff = 0,
                                                        PhaseProf* Pp = nullptr, uint8_t* jobTab = nullptr,
                                                        uint32_t* jobKC = nullptr)
@@ -348,13 +354,13 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
         for (uint32_t i = (uint32_t)lane; i < 272; i += 64) {
             const uint32_t fo = hoff + i, sl = fo >> 2 < 63 ? fo >> 2 : 63u;
             const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * sl), (int)hw->w);
-            sDec.hbuf[i] = (i < nst && i < 144) ? (uint8_t)(v >> (8 * (fo & 3))) : (uint8_t)0;
+            H.hbuf[i] = (i < nst && i < 144) ? (uint8_t)(v >> (8 * (fo & 3))) : (uint8_t)0;
         }
     } else {
-        for (uint32_t i = (uint32_t)lane; i < 272; i += 64) sDec.hbuf[i] = i < nst ? gb(src + i) : (uint8_t)0;
+        for (uint32_t i = (uint32_t)lane; i < 272; i += 64) H.hbuf[i] = i < nst ? gb(src + i) : (uint8_t)0;
     }
     lds_sync();
-    const uint32_t iSize = sDec.hbuf[0];
+    const uint32_t iSize = H.hbuf[0];
     uint32_t nbW = 0;
     size_t used = 0;
     if (iSize >= 128) {
@@ -362,25 +368,25 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
         const uint32_t bytes = (nbW + 1) / 2;
         if (bytes + 1 > srcSize) return 0;
         for (uint32_t nn = 2u * (uint32_t)lane; nn < nbW; nn += 128) {
-            const uint8_t v = sDec.hbuf[1 + nn / 2];
-            sDec.wts[nn] = v >> 4;
-            if (nn + 1 < nbW) sDec.wts[nn + 1] = v & 15;
+            const uint8_t v = H.hbuf[1 + nn / 2];
+            H.wts[nn] = v >> 4;
+            if (nn + 1 < nbW) H.wts[nn + 1] = v & 15;
         }
         used = bytes + 1;
     } else {
         if (iSize + 1 > srcSize) return 0;
         // FSE_readNCount pads a short header with zeros to 8 bytes
-        if (iSize < 8 && (uint32_t)lane < 8 && (uint32_t)lane >= iSize) sDec.hbuf[1 + lane] = 0;
+        if (iSize < 8 && (uint32_t)lane < 8 && (uint32_t)lane >= iSize) H.hbuf[1 + lane] = 0;
         lds_sync();
         unsigned maxSV = z1::kHufTableLogMax, tl = 0;
-        const size_t nc = ncount_lds(sDec.wnorm, &maxSV, &tl, sDec.hbuf + 1, iSize, iSize < 8 ? 8 : iSize, 6);
+        const size_t nc = ncount_lds(H.wnorm, &maxSV, &tl, H.hbuf + 1, iSize, iSize < 8 ? 8 : iSize, 6);
         if (nc == 0 || nc >= iSize) return 0;
         lds_sync();
-        if (!wdtable_build(sDec.wnorm, maxSV, tl)) return 0;
+        if (!wdtable_build(H, H.wnorm, maxSV, tl)) return 0;
         // FSE weight stream: backward bit container over the staged bytes, the decode table in a
         // VGPR (entry u in lane u: newState | symbol << 16 | nbBits << 24, read with v_readlane)
         if (Pp) Pp->mark(12);
-        const uint8_t* bs = sDec.hbuf + 1 + nc;
+        const uint8_t* bs = H.hbuf + 1 + nc;
         const int32_t bl = (int32_t)(iSize - nc);
         const uint32_t last = bs[bl - 1];
         if (last == 0) return 0;
@@ -409,22 +415,22 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
         };
         const uint32_t tsz = 1u << tl;
         const uint32_t E = ((uint32_t)lane < tsz)
-                               ? (uint32_t)sDec.wdt[lane].newState | ((uint32_t)sDec.wdt[lane].symbol << 16) |
-                                     ((uint32_t)sDec.wdt[lane].nbBits << 24)
+                               ? (uint32_t)H.wdt[lane].newState | ((uint32_t)H.wdt[lane].symbol << 16) |
+                                     ((uint32_t)H.wdt[lane].nbBits << 24)
                                : 0u;
         uint32_t st1 = rd(tl), st2 = rd(tl);
         // alternate states; stop when the stream overruns (FSE_decompress_usingDTable tail rule)
         while (true) {
             if (nbW > 253) return 0;
             const uint32_t e1 = readlane_u32(E, (int)st1);
-            sDec.wts[nbW++] = (uint8_t)(e1 >> 16);
+            H.wts[nbW++] = (uint8_t)(e1 >> 16);
             st1 = (e1 & 0xFFFFu) + rd(e1 >> 24);
-            if (pos < 0) { sDec.wts[nbW++] = (uint8_t)(readlane_u32(E, (int)st2) >> 16); break; }
+            if (pos < 0) { H.wts[nbW++] = (uint8_t)(readlane_u32(E, (int)st2) >> 16); break; }
             if (nbW > 253) return 0;
             const uint32_t e2 = readlane_u32(E, (int)st2);
-            sDec.wts[nbW++] = (uint8_t)(e2 >> 16);
+            H.wts[nbW++] = (uint8_t)(e2 >> 16);
             st2 = (e2 & 0xFFFFu) + rd(e2 >> 24);
-            if (pos < 0) { sDec.wts[nbW++] = (uint8_t)(readlane_u32(E, (int)st1) >> 16); break; }
+            if (pos < 0) { H.wts[nbW++] = (uint8_t)(readlane_u32(E, (int)st1) >> 16); break; }
         }
         used = iSize + 1;
     }
@@ -436,7 +442,7 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t sym = 4u * (uint32_t)lane + (uint32_t)q;
-        w4[q] = (sym < nbW) ? sDec.wts[sym] : 0u;
+        w4[q] = (sym < nbW) ? H.wts[sym] : 0u;
         bad |= w4[q] > z1::kHufTableLogMax;
         wsum += w4[q] > z1::kHufTableLogMax ? 0u : ((1u << w4[q]) >> 1);
         r1 += w4[q] == 1;
@@ -458,7 +464,7 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
 #pragma unroll
             for (int qq = 0; qq < 4; qq++) if ((uint32_t)qq == q) w4[qq] = lastWeight;
         }
-        if (lane == 0) sDec.wts[nbW] = (uint8_t)lastWeight;
+        if (lane == 0) H.wts[nbW] = (uint8_t)lastWeight;
     }
     // per-weight counts and exclusive ranks of my four symbols (weights 1..12, 10 bits each)
     uint32_t rankIdx[4] = {0, 0, 0, 0};
@@ -503,10 +509,10 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t sym = 4u * (uint32_t)lane + (uint32_t)q;
-        if (sym < nbSym && w4[q]) sDec.order[before[w4[q]] + rankIdx[q]] = (uint8_t)sym;
+        if (sym < nbSym && w4[q]) H.order[before[w4[q]] + rankIdx[q]] = (uint8_t)sym;
     }
     lds_sync();
-    if (jobTab) {
+    if (JobOnly || jobTab) {
         // dec_frame_fast: the job's compact table (pgn_hufjob.h) straight from the ranks, without the
         // 2^tl-entry table.  Entries with codes longer than K = tl - d are those of weights <= d, the
         // first rankStart[d + 1] of the table; entry idx belongs to the last weight whose range starts
@@ -536,7 +542,7 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
                 rs0 = in ? rankStart[ww] : rs0;
                 bf = in ? before[ww] : bf;
             }
-            const uint32_t sym = sDec.order[bf + ((idx - rs0) >> (w - 1))];
+            const uint32_t sym = H.order[bf + ((idx - rs0) >> (w - 1))];
             gst<uint16_t>(jobTab + 2 * j, (uint16_t)((tl + 1 - w) | (sym << 8)));
         }
         jobKC[0] = K;
@@ -548,6 +554,7 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
         *minNbOut = tl + 1 - wave_max(wmx);
         return used;
     }
+    if constexpr (JobOnly) return 0;
     // fill weight by weight: weight w owns entries [rankStart[w], rankStart[w] + cntW[w] << (w - 1))
 #pragma unroll
     for (unsigned w = 1; w <= 12; w++) {
@@ -555,7 +562,7 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
         const uint32_t a = rankStart[w], end = a + (cntW[w] << (w - 1));
         const uint16_t nbb = (uint16_t)((tl + 1 - w) << 8);
         for (uint32_t u = a + (uint32_t)lane; u < end; u += 64) {
-            const uint16_t e = (uint16_t)(sDec.order[before[w] + ((u - a) >> (w - 1))] | nbb);
+            const uint16_t e = (uint16_t)(H.order[before[w] + ((u - a) >> (w - 1))] | nbb);
             if (tl <= kHufLdsLog) sDec.tab[u] = e;
             else gst<uint16_t>(gt + u, e);
         }
@@ -573,7 +580,7 @@ __device__ __forceinline__ size_t huf_build_dtable_body(const uint8_t* src, size
 __device__ __noinline__ size_t huf_build_dtable_wave(const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
                                                      unsigned* minNbOut)
 {
-    return huf_build_dtable_body(src, srcSize, tlOut, gt, minNbOut);
+    return huf_build_dtable_body<false>(sDec.hb, src, srcSize, tlOut, gt, minNbOut);
 }
 
 }  // namespace pgn
@@ -1200,7 +1207,7 @@ __device__ __noinline__ long zstd_decompress_wave(const uint8_t* __restrict__ sr
 // are the general decoder's in every case.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, size_t srcSize, uint8_t* __restrict__ dst,
-                                               size_t dstCap, uint8_t* job, uint16_t* htab, PhaseProf& P)
+                                               size_t dstCap, uint8_t* job, uint16_t* htab, PhaseProf& P, HufBuildLds& H)
 {
     if (srcSize < 9) return -1;
     HdrWin hw;
@@ -1243,7 +1250,7 @@ __device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, 
     const uint8_t* hp = src + ip + lh;
     unsigned tl = 0, mn = 1;
     uint32_t kc[2] = {0, 0};
-    const size_t hsz = huf_build_dtable_body(hp, cs, &tl, htab, &mn, &hw, (uint32_t)(ip + lh), &P, job + sizeof(HufJob), kc);
+    const size_t hsz = huf_build_dtable_body<true>(H, hp, cs, &tl, htab, &mn, &hw, (uint32_t)(ip + lh), &P, job + sizeof(HufJob), kc);
     P.mark(1);
     if (hsz == 0 || tl > kHufLdsLog || cs - hsz < 6) return -1;
     hp += hsz;
