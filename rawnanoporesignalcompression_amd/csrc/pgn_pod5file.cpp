@@ -1431,6 +1431,7 @@ int pgn_pod5_write_file_keep_going(const char* path, const pgn_pod5_file* source
                                    const uint8_t* section_marker, pgn_pod5_keep_going_result* res)
 {
     if (!path || (rows && (!read_ids || !samples || !offsets || !row_status))) return PGN_ERR_INVALID_ARG;
+    if (rows && offsets[rows] > offsets[0] && !data) return PGN_ERR_INVALID_ARG;  // as pgn_pod5_write_file
     return guarded([&] {
         pgn_pod5_keep_going_result r{0, 0, 0, 0, UINT64_MAX, 0, 0};
         std::vector<uint8_t> keepRow(rows, 0);
@@ -1497,8 +1498,14 @@ int pgn_pod5_write_file_keep_going(const char* path, const pgn_pod5_file* source
                 for (const auto& rl : lists)
                     for (int64_t row : rl) listed[row] = 1;
             }
-            for (uint64_t i = 0; i < rows; i++)
+            for (uint64_t i = 0; i < rows; i++) {
                 if (!listed[i] && row_status[i] == 0) keepRow[i] = 1;
+                // a failing row no read lists is dropped too: reported like the listed ones
+                if (!listed[i] && row_status[i] != 0 && r.first_failed_row == UINT64_MAX) {
+                    r.first_failed_row = i;
+                    r.first_status = row_status[i];
+                }
+            }
         } else {  // no reads table: every row stands alone
             for (uint64_t i = 0; i < rows; i++) {
                 keepRow[i] = row_status[i] == 0;
