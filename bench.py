@@ -151,7 +151,7 @@ def rank_batches(args, rank: int, world: int):
     return mine, [base + (1 if i < extra else 0) for i in range(nb)], "strong"
 
 
-# ---- CPU baselines (the oracle: test infrastructure, timed as the reference's CPU path) -----------
+# ---- CPU baselines (the oracle, a C restatement of C5.hpp over libzstd: test infrastructure, timed as the CPU baseline) ---
 def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
