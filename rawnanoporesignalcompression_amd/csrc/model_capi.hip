@@ -93,6 +93,17 @@ long z1m_decompress(const uint8_t* src, size_t n, uint8_t* dst, size_t cap)
     return r;
 }
 
+// HUF_buildCTable's code lengths for a histogram (maxNbBits 11): decode-table size studies.
+unsigned z1m_huf_lengths(const uint32_t* count, unsigned maxSymbolValue, uint8_t* nbBits)
+{
+    HufNode* nodes = (HufNode*)calloc(1024, sizeof(HufNode));
+    huf_sort_serial(nodes + 1, count, maxSymbolValue);
+    uint16_t val[256];
+    const unsigned r = huf_build_from_sorted(nodes, maxSymbolValue, 11, nbBits, val);
+    free(nodes);
+    return r;
+}
+
 long long z1m_content_size(const uint8_t* src, size_t n)
 {
     bool ok = false;

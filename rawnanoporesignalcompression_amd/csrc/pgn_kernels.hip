@@ -523,8 +523,9 @@ __device__ inline int over_claim_status(const uint8_t* in, const DecUnit* u, con
 }
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586).
-// Frames claiming more content than the intermediate holds (interCap = 5 capN bytes, capN >= every
-// chunk of the call) or a stream above kPassSamples are PGN_ERR_UNSUPPORTED (include/pgnano_hip.h).
+// Frames claiming more content than the intermediate holds (inter_cap(capN) = 2.25 capN + 1,024
+// bytes, capN >= every chunk of the call), or one frame more than kPassSamples bytes, get
+// over_claim_status.
 __device__ inline int c5_parse_chunk(const uint8_t* in, uint64_t src0, uint64_t len, DecUnit* u, size_t interCap)
 {
     const uint8_t* src = in + src0;
@@ -652,7 +653,14 @@ constexpr int kHufFrames = 16;
 constexpr uint32_t kPf = PGN_K2_PF;             // iterations between a block load and its staging
 constexpr uint32_t kRing = 16 * kPf;            // dwords per lane (4 kPf blocks)
 constexpr uint32_t kRingBlocks = kRing / 4;
+#if PGN_K2_DIAG == 4  // diagnostic (wrong output): 256-entry tables (occupancy probe, PGN_K2_PAD sets the LDS)
+constexpr uint32_t kTabStride = 256;
+#else
 constexpr uint32_t kTabStride = kJobTabUse;     // LDS table entries per frame
+#endif
+#ifndef PGN_K2_PAD
+#define PGN_K2_PAD 0
+#endif
 constexpr uint32_t kZeroTab = 16;               // frozen lanes' table entries
 constexpr size_t kHufJunkBytes = 64 * 128;      // frozen lanes' store target: a line per lane, shared by all waves
 static_assert((2 * kTabStride) % 16 == 0, "frame tables stay 16-byte aligned");
@@ -683,6 +691,13 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     __shared__ __attribute__((aligned(16))) uint16_t tabs[kHufFrames * kTabStride + kZeroTab];
     __shared__ uint32_t ring[kRing * 64];
     const uint32_t lane = (uint32_t)lane_id();
+#if PGN_K2_PAD > 0
+    __shared__ uint32_t kpad[PGN_K2_PAD / 4];
+    if (a.G == ~(size_t)0) {  // never taken; a load keeps the array (and its LDS) alive
+        kpad[lane] = lane;
+        a.status[lane] = (int32_t)kpad[lane ^ 1u];
+    }
+#endif
     const size_t G = a.G;
     const uint32_t ngrp = (uint32_t)((G + kHufFrames - 1) / kHufFrames);
     const uint32_t kq = blockIdx.x / ngrp;  // queue position: the large streams' groups first
@@ -713,7 +728,7 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
         }
 #pragma unroll
         for (int ff = 0; ff < kHufFrames; ff++)
-            if (lane < 63) *(uint4*)&tabs[ff * kTabStride + 8 * lane] = tv[ff];
+            if (lane < (kTabStride < 504 ? kTabStride / 8 : 63)) *(uint4*)&tabs[ff * kTabStride + 8 * lane] = tv[ff];
         if (lane < kZeroTab / 2) ((uint32_t*)&tabs[kHufFrames * kTabStride])[lane] = 0u;
     }
     uint8_t* const junk = a.jobs + G * kStreams * kJobBytes + 128 * lane;
@@ -821,6 +836,9 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
         const uint32_t a1 = ((hi >> s1) + tb) << 1, a2 = ((hi >> sh2) + tc) << 1;
 #if PGN_K2_DIAG == 3  // diagnostic (wrong output): the table read replaced by arithmetic on the peek
         const uint32_t ent = ((a1 < a2 ? a1 : a2) & 0xFF00u) | (4u + (hi >> 30));
+#elif PGN_K2_DIAG == 4  // 256-entry tables: two more VALU per symbol
+        const uint32_t am = a1 < a2 ? a1 : a2;
+        const uint32_t ent = *(const uint16_t*)((const uint8_t*)tabs + (((am - 2 * tb) & 511u) + 2 * tb));
 #else
         const uint32_t ent = *(const uint16_t*)((const uint8_t*)tabs + (a1 < a2 ? a1 : a2));
 #endif
@@ -1045,7 +1063,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void de
     static __shared__ MergeLds W;
     PhaseProf P;
     P.init(a.prof);
-    const DecUnit* d = a.units + g * kStreams;
+#if PGN_MERGE_DIAG == 1  // diagnostic: chunk g merges chunk g % 32's intermediate (L2-resident reads, same work on equal-size chunks)
+    const size_t gi = g % 32;
+#else
+    const size_t gi = g;
+#endif
+    const DecUnit* d = a.units + gi * kStreams;
     uint64_t total = 0;
     int st = PGN_OK;
     for (int s = 0; s < kStreams; s++) {
@@ -1054,7 +1077,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void de
     }
     if (st == PGN_OK) {
         uint64_t consumed = 0;
-        const int bad = c5_merge_wave(a.inter + g * a.interStride, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres,
+        const int bad = c5_merge_wave(a.inter + gi * a.interStride, total, (uint64_t)d[1].dres, (uint64_t)d[2].dres,
                                       (uint64_t)d[3].dres, a.samples + a.sampleOffsets[c], a.sampleCounts[c], &consumed, W);
         if (bad) st = PGN_ERR_CORRUPT;
         else if (consumed != total) st = PGN_ERR_REMAINING;
@@ -1082,7 +1105,12 @@ __global__ __launch_bounds__(64) void dec_merge_lb_kernel(DecArgs a)
     if (g >= a.G || c >= a.nchunks) return;
     if (a.status[c] != PGN_OK) return;
     const uint32_t lane = (uint32_t)lane_id();
-    const DecUnit* d = a.units + g * kStreams;
+#if PGN_MERGE_DIAG == 1  // diagnostic: chunk g merges chunk g % 32's intermediate (L2-resident reads, same work on equal-size chunks)
+    const size_t gi = g % 32;
+#else
+    const size_t gi = g;
+#endif
+    const DecUnit* d = a.units + gi * kStreams;
     uint64_t total = 0;
     int st = PGN_OK;
     for (int s = 0; s < kStreams; s++) {
@@ -1790,10 +1818,12 @@ struct pgn_ctx {
     hipStream_t mergeS = nullptr;
     hipEvent_t evHuf[2] = {nullptr, nullptr};
     // decode passes: buffers in rotation (PGN_DEC_BUFS, 2..kMaxDecBufs) with their stage / sections /
-    // free events, and the streams the deferred sections alternate over (PGN_HUF_STREAMS, 1 or 2)
-    // measured (tools/gpu_env_sweep.sh, 100,000 chunks): 2 buffers / 1 stream / passes of 20,000:
-    // decode 23.1 ms; 4 / 2 / 12,500: 22.7 ms (profiles/r05_decode_pipeline_sweep.log)
-    size_t decBufs = 4, hufStreams = 2;
+    // free events, and the streams the deferred sections alternate over (PGN_HUF_STREAMS: 1 or 2 with
+    // the merges on mergeS; 3 = sections and merge of pass p both on side stream p % 3 of side, side2,
+    // mergeS).  Measured (tools/gpu_env_sweep.sh, 100,000 chunks): 2 buffers / 1 stream / passes of
+    // 20,000: decode 23.1 ms; 4 / 2 / 12,500: 22.7 ms; 4 / 3 / 12,500: 22.3-22.6 ms against 22.8-23.1
+    // in interleaved A/B (profiles/r05_decode_pipeline_sweep.log)
+    size_t decBufs = 4, hufStreams = 3;
     hipStream_t side2 = nullptr;
     hipEvent_t evDStage[kMaxDecBufs] = {}, evDHuf[kMaxDecBufs] = {}, evDFree[kMaxDecBufs] = {};
     uint64_t* prof = nullptr;  // kProfWords: phase cycles and counters (encode, decode, dec_huf) when PGN_PHASE_PROFILE=1
@@ -1935,7 +1965,10 @@ int pgn_ctx_create(int device, pgn_ctx** out)
         const long x = atol(v);
         if (x >= 2 && x <= kMaxDecBufs) c->decBufs = (size_t)x;
     }
-    if (const char* v = getenv("PGN_HUF_STREAMS")) c->hufStreams = atol(v) == 2 ? 2 : 1;
+    if (const char* v = getenv("PGN_HUF_STREAMS")) {
+        const long x = atol(v);
+        c->hufStreams = x >= 1 && x <= 3 ? (size_t)x : c->hufStreams;
+    }
     HIPCHK(hipStreamCreateWithFlags(&c->scanStream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->evScanFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->evScan, hipEventDisableTiming));
@@ -2339,7 +2372,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
 #endif
     // deferred sections over several passes: the sections of pass p on hufS[p % hufStreams], the merges
     // on a third stream behind them
-    const hipStream_t hufS[2] = {c->side, c->side2};
+    // 3: the sections and the merge of pass p both on side stream p % 3 (no separate merge stream)
+    const hipStream_t hufS[3] = {c->side, c->side2, c->mergeS};
     const size_t hufStreams = c->hufStreams;
     if (passes > 1) {
         HIPCHK(hipEventRecord(c->evFork, s));
@@ -2400,7 +2434,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         // with deferred sections over several passes the merge goes to the third stream behind its
         // pass's sections (so it overlaps the next pass's sections); the buffer is free after it
         hipStream_t ms = hs;
-        if (defer && multi) {
+        if (defer && multi && hufStreams < 3) {
             HIPCHK(hipEventRecord(c->evDHuf[b], hs));
             HIPCHK(hipStreamWaitEvent(c->mergeS, c->evDHuf[b], 0));
             ms = c->mergeS;
@@ -2412,7 +2446,9 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         if (passes > 1) HIPCHK(hipEventRecord(c->evDFree[b], ms));
     }
     HIPCHK(hipGetLastError());
-    if (multi) {  // the last merge follows every other launch of the call on the side streams
+    if (multi && defer && hufStreams == 3) {  // every buffer's last merge (each follows its pass's sections)
+        for (size_t b = 0; b < nbuf; b++) HIPCHK(hipStreamWaitEvent(s, c->evDFree[b], 0));
+    } else if (multi) {  // the last merge follows every other launch of the call on the side streams
         HIPCHK(hipEventRecord(c->evJoin, defer ? c->mergeS : c->side));
         HIPCHK(hipStreamWaitEvent(s, c->evJoin, 0));
     }
