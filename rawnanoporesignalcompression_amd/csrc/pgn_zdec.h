@@ -747,6 +747,116 @@ __device__ __forceinline__ uint32_t seqbits_read(SeqBits& b, uint32_t nb)
     return (uint32_t)(b.C >> (lo - b.cl)) & (uint32_t)((1ull << nb) - 1ull);
 }
 
+// The execution of a frame's first block when all its sequences (nb <= 64, decoded into sDec.qsq) are
+// one batch (on the C5 data the Lhigh frame: ~18 sequences, ~1.2 KB): the checks exec_sequences_wave's
+// loop makes per sequence, for all of them at once (the first failing sequence's first failing check
+// wins, as in the loop; then a bitstream not consumed to its first bit, brBad; then the trailing
+// literals' room).  A block that fits runs in LDS -- literals staged into the freed bitstream window,
+// the output built in the freed FSE tables, matches copied LDS to LDS, one store pass at the end --
+// instead of a global-memory round trip per literal run and per match; a larger one runs the loop's
+// global-memory copies.  A call in tail position, so the caller keeps nothing live across it (its
+// registers bound the decode kernels' occupancy).  Returns the new output position or a DecErr.
+__device__ __noinline__ long exec_one_batch(const uint8_t* lit, size_t rs, uint8_t* dst, size_t op, size_t dstCap,
+                                            uint32_t nb, bool brBad)
+{
+    const int lane = lane_id();
+    lit = uni(lit);
+    rs = uni((uint64_t)rs);
+    dst = uni(dst);
+    op = uni((uint64_t)op);
+    dstCap = uni((uint64_t)dstCap);
+    nb = uni(nb);
+    {
+        const bool in = (uint32_t)lane < nb;
+        const uint32_t sll = in ? sDec.qsq[lane][0] : 0u, sml = in ? sDec.qsq[lane][1] : 0u;
+        const uint32_t sof = in ? sDec.qsq[lane][2] : 0u;
+        const uint32_t llIncl = wave_incl_sum(sll), outIncl = wave_incl_sum(sll + sml);
+        const uint32_t o0 = outIncl - sll - sml;      // this sequence's output offset in the block
+        const bool e1 = in && (size_t)llIncl > rs;    // literals beyond the section
+        const bool e2 = in && op + outIncl > dstCap;  // output beyond the destination
+        const bool e3 = in && sof > o0 + sll;         // match before the frame start
+        const uint64_t em = ballot(e1 || e2 || e3);
+        if (em) {
+            const int ft = (int)__builtin_ctzll(em);
+            return readlane_u32(e1 ? 1u : (e2 ? 2u : 3u), ft) == 2u ? (long)z1::kDecErrDstSmall : (long)z1::kDecErrCorrupt;
+        }
+        if (brBad) return z1::kDecErrCorrupt;
+        const size_t remLit = rs - readlane_u32(llIncl, 63);
+        const uint32_t totOut = readlane_u32(outIncl, 63);
+        if (op + totOut + remLit > dstCap) return z1::kDecErrDstSmall;
+        constexpr uint32_t kOut = 4096;  // output bytes held in sDec.qtab (5,120 B)
+        if ((size_t)totOut + remLit > kOut || rs > (size_t)kSeqWin) {  // too large for LDS: global copies
+            size_t o = op, litPos = 0;
+            for (uint32_t t = 0; t < nb; t++) {
+                const uint32_t ll = sDec.qsq[t][0], ml = sDec.qsq[t][1], off = sDec.qsq[t][2];
+                wave_copy(dst + o, lit + litPos, ll);
+                litPos += ll;
+                o += ll;
+                lds_sync();
+                if (off >= 64 || off >= ml) {
+                    for (uint32_t k = (uint32_t)lane; k < ml; k += 64) gst<uint8_t>(dst + o + k, gb(dst + o - off + k));
+                } else {
+                    uint32_t r = (uint32_t)lane % off;
+                    const uint32_t adv = 64u % off;
+                    for (uint32_t k = (uint32_t)lane; k < ml; k += 64) {
+                        gst<uint8_t>(dst + o + k, gb(dst + o - off + r));
+                        r += adv;
+                        r = r >= off ? r - off : r;
+                    }
+                }
+                o += ml;
+                lds_sync();
+            }
+            wave_copy(dst + o, lit + litPos, rs - litPos);
+            o += rs - litPos;
+            lds_sync();
+            return (long)o;
+        }
+    }
+    uint8_t* const ob = (uint8_t*)sDec.qtab;
+    uint8_t* const lb = sDec.qwin;
+    const uint32_t n = (uint32_t)rs;
+    for (uint32_t i = (uint32_t)lane * 16; i < n; i += 1024) {
+        if (i + 16 <= n) {
+            *(uint4*)(lb + i) = gld<uint4>(lit + i);
+        } else {
+            for (uint32_t k = i; k < n; k++) lb[k] = gb(lit + k);
+        }
+    }
+    lds_sync();
+    uint32_t o = 0, lp = 0;
+    for (uint32_t t = 0; t < nb; t++) {
+        const uint32_t ll = sDec.qsq[t][0], ml = sDec.qsq[t][1], off = sDec.qsq[t][2];
+        for (uint32_t k = (uint32_t)lane; k < ll; k += 64) ob[o + k] = lb[lp + k];
+        o += ll;
+        lp += ll;
+        lds_sync();
+        if (off >= 64 || off >= ml) {  // no overlap within a 64-byte step
+            for (uint32_t k = (uint32_t)lane; k < ml; k += 64) {
+                ob[o + k] = ob[o - off + k];
+                lds_sync();
+            }
+        } else {  // repeating pattern of period off
+            uint32_t r = (uint32_t)lane % off;
+            const uint32_t adv = 64u % off;
+            for (uint32_t k = (uint32_t)lane; k < ml; k += 64) {
+                ob[o + k] = ob[o - off + r];
+                r += adv;
+                r = r >= off ? r - off : r;
+                lds_sync();
+            }
+        }
+        o += ml;
+        lds_sync();
+    }
+    for (uint32_t k = (uint32_t)lane; k < n - lp; k += 64) ob[o + k] = lb[lp + k];
+    o += n - lp;
+    lds_sync();
+    for (uint32_t i = (uint32_t)lane; i < o; i += 64) gst<uint8_t>(dst + op + i, ob[i]);
+    lds_sync();
+    return (long)(op + o);
+}
+
 // One block's sequences: decode + execute.  Returns the new output position or a negative DecErr.
 __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t seqSize, const uint8_t* lit, size_t rs,
                                                  uint8_t* dst, size_t op, size_t dstCap, size_t frameStart,
@@ -892,6 +1002,17 @@ __device__ __noinline__ long exec_sequences_wave(const uint8_t* seqSrc, size_t s
             }
             lds_sync();
             P.mark(13);
+#ifndef PGN_SEQ_LDS_OFF
+            if (nbSeq <= 64 && op == frameStart) {  // a frame's first block, one batch: the rest is exec_one_batch's
+                fs.rep0 = rep0;
+                fs.rep1 = rep1;
+                fs.rep2 = rep2;
+                fs.valid = valid;
+                const long r = exec_one_batch(lit, rs, dst, op, dstCap, nb, br.pos != 0);
+                P.mark(15);
+                return r;
+            }
+#endif
             // execute the batch
             for (uint32_t t = 0; t < nb; t++) {
                 const uint32_t ll = sDec.qsq[t][0], ml = sDec.qsq[t][1], off = sDec.qsq[t][2];
