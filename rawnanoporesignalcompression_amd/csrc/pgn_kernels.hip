@@ -667,9 +667,7 @@ static_assert((2 * kTabStride) % 16 == 0, "frame tables stay 16-byte aligned");
 
 __device__ __forceinline__ uint64_t shl64(uint64_t c, uint32_t e)  // c << (e & 63), one v_lshlrev_b64
 {
-    uint64_t r;
-    asm volatile("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "v"(e), "v"(c));
-    return r;
+    return c << (e & 63u);
 }
 __device__ __forceinline__ uint32_t cnd(bool c, uint32_t a, uint32_t b)  // c ? a : b, one v_cndmask
 {
@@ -776,14 +774,20 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     const uint32_t v0 = live ? (uint32_t)(e & 3u) * 8u + hb : 0u;  // valid bits of the top dword
     const uint32_t totalBits = sl ? (sl - 1) * 8u + hb : 0u;
     const uint32_t ins0 = 4 - i0;  // ring position of the dword below the top one
-    uint32_t ins = ins0, avail = v0;
+    // insb: the ring position of the next dword times 256 (its slot's byte offset in the ring, before
+    // the wrap), so a refill advances it and forms the LDS address with one instruction each
+    uint32_t insb = ins0 << 8, avail = v0;
+    const uint32_t laneOff = 4u * lane;
+    auto ring_at = [&](uint32_t ib) -> uint32_t {  // ring[64 * ((ib >> 8) & (kRing - 1)) + lane]
+        return *(const uint32_t*)((const uint8_t*)ring + ((ib & ((kRing - 1) << 8)) | laneOff));
+    };
     uint64_t C;
     uint32_t nd;
     // blocks in flight: slot 0 was loaded kPf iterations ago (staged next), slot kPf - 1 last
     uint4 La[kPf], Lb[kPf];
     uint32_t lb[kPf];  // block of La (Lb: lb + 1)
     auto issue = [&](uint32_t slot) {
-        lb[slot] = (ins >> 2) + 2 * kPf;
+        lb[slot] = (insb >> 10) + 2 * kPf;
         La[slot] = blk(lb[slot]);
         Lb[slot] = blk(lb[slot] + 1);
     };
@@ -803,16 +807,16 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
         C = v0 ? ((uint64_t)dw0 << (64 - v0)) : 0ull;
         // first refill (avail <= 31), and a second one when the container still holds only 32
         // bits: every pair of symbols starts with at least 33
-        nd = ring[64 * (ins & (kRing - 1)) + lane];
+        nd = ring_at(insb);
         C |= shl64((uint64_t)nd, 32u - avail);
         avail += 32;
-        ins++;
-        nd = ring[64 * (ins & (kRing - 1)) + lane];
+        insb += 256;
+        nd = ring_at(insb);
         if (avail <= 32) {
             C |= (uint64_t)nd;
             avail += 32;
-            ins++;
-            nd = ring[64 * (ins & (kRing - 1)) + lane];
+            insb += 256;
+            nd = ring_at(insb);
         }
     }
     // refill check: the dword goes into Cadd, which the next symbol ORs into the container only
@@ -820,12 +824,12 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     // with at least 33 bits and takes at most 22), so the refill is off the symbols' latency chain
     uint64_t Cadd = 0;
     auto refill = [&]() {
-        const bool m = avail <= 32;
-        const uint32_t x = m ? nd : 0u;
+        const uint32_t m01 = avail <= 32 ? 1u : 0u;
+        const uint32_t x = m01 ? nd : 0u;
         Cadd = shl64((uint64_t)x, 32u - avail);
-        avail += m ? 32u : 0u;
-        ins += m ? 1u : 0u;
-        nd = ring[64 * (ins & (kRing - 1)) + lane];
+        avail += m01 << 5;  // one v_lshl_add each
+        insb += m01 << 8;
+        nd = ring_at(insb);
     };
     // table byte addresses: entry min(p, pq) of the lane's table, p = peek >> (32 - tl),
     // pq = (peek >> (32 - K)) + Cc; tb / tc carry the table base (the zero table when frozen)
@@ -970,7 +974,7 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
         gst<uint8_t>(sdst + i, (uint8_t)(ent >> 8));
     }
     // exact end: the stream's bits consumed to its first bit
-    if (live) bad = (v0 + 32u * (ins - ins0) - avail) != totalBits;
+    if (live) bad = (v0 + 32u * ((insb >> 8) - ins0) - avail) != totalBits;
     const uint64_t bm = ballot(bad);
     if (q == 0 && flag && ((bm >> (4 * f)) & 0xFull)) gst<int32_t>(&a.units[g * kStreams + (size_t)s].dres, (int32_t)z1::kDecErrHufStream);
     Pp.mark(3);  // drain, head / tail bytes, the last symbols, the end check
