@@ -11,14 +11,13 @@
 // one lane's stream is ~16k symbols long, so it only pays with thousands of frames in flight
 // (launch_decode_impl uses it for large passes).
 //
-// Compact table (LDS budget: 16 frames x 1 KiB per wave).  zstd's single-symbol table (HUF_readDTableX1)
-// has 2^tl entries; codes longer than K bits are canonical and occupy the low indices [0, T) (weight 1
-// first), codes of at most K bits repeat every entry 2^(tl-K) times above T.  Keeping [0, T) whole and
-// one entry per 2^(tl-K) above it, the entry of a peek p (the stream's next tl bits) is
-//     idx = min(p, (p >> (tl - K)) + Cc),   Cc = T - (T >> (tl - K))
-// (both arguments are monotone in p and cross at T).  K is chosen per table for the smallest size;
-// a table of more than 504 entries (never seen on zstd level-1 output: 400-480 on the bench's keys /
-// M frames) is decoded in place by the frame decoder as before.
+// Compact table (LDS budget: 16 frames x 704 B per wave).  zstd's single-symbol table (HUF_readDTableX1)
+// has 2^tl entries; longer codes are canonical and occupy the low indices (weight 1 first), a code of
+// length L repeats over 2^(tl-L) entries.  The job keeps three segments of the table at three
+// resolutions (pgn_zdec.h job_segments): the entry of a peek p (the stream's next tl bits) is
+//     idx = min(p, (p >> d1) + C1, (p >> d2) + C2)
+// (round 4 kept two segments, min(p, (p >> d) + Cc): 400-480 entries on the bench's keys / M frames,
+// now 190-345).  A table of more than kJobTabUse = 352 entries is decoded in place by the frame decoder.
 #pragma once
 // included by pgn_zdec.h (after the Huffman table builder; sDec, kHufLdsLog)
 
@@ -31,9 +30,10 @@ struct HufJob {
     uint64_t dst;     // rs literals (stream k: seg = (rs + 3) / 4 of them at dst + k seg; the last rs - 3 seg)
     uint32_t len[4];  // stream bytes
     uint32_t rs;
-    uint32_t tl, K, Cc;
-    uint32_t flag;    // 1: pending for dec_huf_kernel (written for every unit of a pass)
-    uint32_t pad[3];
+    uint32_t tl, dd, C1;  // table log; d1 | d2 << 8; C1 (the compact table's segments)
+    uint32_t flag;        // 1: pending for dec_huf_kernel (written for every unit of a pass)
+    uint32_t C2;
+    uint32_t pad[2];
 };
 static_assert(sizeof(HufJob) == 64, "HufJob header");
 constexpr size_t kJobBytes = sizeof(HufJob) + 2 * kJobTab;
@@ -59,35 +59,22 @@ __device__ __forceinline__ bool huf_defer_body(uint8_t* job, unsigned tl, const 
     const uint32_t l4 = (uint32_t)(remain - 6 - l1 - l2 - l3);
     const uint32_t seg = (rs + 3) / 4;
     if (seg * 3 > rs || tl < 1 || tl > kHufLdsLog) return false;
-    // T_K for K = tl - 1 .. tl - 4: table entries whose code is longer than K bits
-    uint32_t c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+    // T[d] for d = 0 .. 7: table entries whose code is longer than tl - d bits
+    uint32_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const uint32_t tsz = 1u << tl;
     for (uint32_t u = lane; u < tsz; u += 64) {
         const uint32_t nb = sDec.tab[u] >> 8;
-        c1 += nb + 1 > tl;
-        c2 += nb + 2 > tl;
-        c3 += nb + 3 > tl;
-        c4 += nb + 4 > tl;
-    }
-    const uint32_t T1 = wave_sum(c1), T2 = wave_sum(c2), T3 = wave_sum(c3), T4 = wave_sum(c4);
-    uint32_t K = tl, T = 0, size = tsz;
-    const uint32_t Ts[4] = {T1, T2, T3, T4};
 #pragma unroll
-    for (uint32_t d = 1; d <= 4; d++) {
-        if (d >= tl) break;
-        const uint32_t t = Ts[d - 1], sz = t + ((tsz - t) >> d);
-        if (sz < size) {
-            size = sz;
-            K = tl - d;
-            T = t;
-        }
+        for (uint32_t d = 1; d < 8; d++) cnt[d] += nb + d > tl;
     }
-    if (size > kJobTabUse) return false;
-    const uint32_t d = tl - K;
-    const uint32_t Cc = T - (T >> d);
+    uint32_t Td[8];
+#pragma unroll
+    for (int d = 0; d < 8; d++) Td[d] = wave_sum(cnt[d]);
+    const JobSeg sg = job_segments(Td, tl);
+    if (sg.size > kJobTabUse) return false;
     uint16_t* tab = (uint16_t*)(job + sizeof(HufJob));
-    for (uint32_t j = lane; j < size; j += 64) {
-        const uint32_t e = sDec.tab[j < T ? j : (j - Cc) << d];
+    for (uint32_t j = lane; j < sg.size; j += 64) {
+        const uint32_t e = sDec.tab[job_entry_index(sg, j)];
         gst<uint16_t>(tab + j, (uint16_t)((e >> 8) | ((e & 0xFFu) << 8)));
     }
     HufJob* J = (HufJob*)job;
@@ -95,15 +82,16 @@ __device__ __forceinline__ bool huf_defer_body(uint8_t* job, unsigned tl, const 
         gst<uint64_t>(&J->hp, (uint64_t)hp);
         gst<uint64_t>(&J->dst, (uint64_t)dst);
         gst<uint4>(&J->len[0], make_uint4(l1, l2, l3, l4));
-        gst<uint4>(&J->rs, make_uint4(rs, tl, K, Cc));
+        gst<uint4>(&J->rs, make_uint4(rs, tl, sg.d1 | (sg.d2 << 8), sg.C1));
+        gst<uint32_t>(&J->C2, sg.C2);
         gst<uint32_t>(&J->flag, 1u);
     }
     return true;
 }
 // The job header alone (dec_frame_fast writes the compact table itself, from the table build's ranks):
-// the same checks and fields as huf_defer_body, K / Cc given.
+// the same checks and fields as huf_defer_body, the segments given (kc: d1 | d2 << 8, C1, C2).
 __device__ __forceinline__ bool huf_defer_header(uint8_t* job, unsigned tl, const uint8_t* hp, size_t remain, uint8_t* dst,
-                                                 uint32_t rs, uint32_t jt01, uint32_t jt2, uint32_t K, uint32_t Cc)
+                                                 uint32_t rs, uint32_t jt01, uint32_t jt2, const uint32_t (&kc)[3])
 {
     const uint32_t lane = (uint32_t)lane_id();
     const uint32_t l1 = jt01 & 0xFFFFu, l2 = jt01 >> 16, l3 = jt2;
@@ -116,7 +104,8 @@ __device__ __forceinline__ bool huf_defer_header(uint8_t* job, unsigned tl, cons
         gst<uint64_t>(&J->hp, (uint64_t)hp);
         gst<uint64_t>(&J->dst, (uint64_t)dst);
         gst<uint4>(&J->len[0], make_uint4(l1, l2, l3, l4));
-        gst<uint4>(&J->rs, make_uint4(rs, tl, K, Cc));
+        gst<uint4>(&J->rs, make_uint4(rs, tl, kc[0], kc[1]));
+        gst<uint32_t>(&J->C2, kc[2]);
         gst<uint32_t>(&J->flag, 1u);
     }
     return true;

@@ -653,14 +653,7 @@ constexpr int kHufFrames = 16;
 constexpr uint32_t kPf = PGN_K2_PF;             // iterations between a block load and its staging
 constexpr uint32_t kRing = 16 * kPf;            // dwords per lane (4 kPf blocks)
 constexpr uint32_t kRingBlocks = kRing / 4;
-#if PGN_K2_DIAG == 4  // diagnostic (wrong output): 256-entry tables (occupancy probe, PGN_K2_PAD sets the LDS)
-constexpr uint32_t kTabStride = 256;
-#else
 constexpr uint32_t kTabStride = kJobTabUse;     // LDS table entries per frame
-#endif
-#ifndef PGN_K2_PAD
-#define PGN_K2_PAD 0
-#endif
 constexpr uint32_t kZeroTab = 16;               // frozen lanes' table entries
 constexpr size_t kHufJunkBytes = 64 * 128;      // frozen lanes' store target: a line per lane, shared by all waves
 static_assert((2 * kTabStride) % 16 == 0, "frame tables stay 16-byte aligned");
@@ -689,13 +682,6 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     __shared__ __attribute__((aligned(16))) uint16_t tabs[kHufFrames * kTabStride + kZeroTab];
     __shared__ uint32_t ring[kRing * 64];
     const uint32_t lane = (uint32_t)lane_id();
-#if PGN_K2_PAD > 0
-    __shared__ uint32_t kpad[PGN_K2_PAD / 4];
-    if (a.G == ~(size_t)0) {  // never taken; a load keeps the array (and its LDS) alive
-        kpad[lane] = lane;
-        a.status[lane] = (int32_t)kpad[lane ^ 1u];
-    }
-#endif
     const size_t G = a.G;
     const uint32_t ngrp = (uint32_t)((G + kHufFrames - 1) / kHufFrames);
     const uint32_t kq = blockIdx.x / ngrp;  // queue position: the large streams' groups first
@@ -717,7 +703,7 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     // the pending frames' compact tables (kTabStride entries each, 16 bytes per lane; all loads in
     // flight at once)
     {
-        const uint32_t lt = lane < 63 ? lane : 62;
+        const uint32_t lt = lane < kTabStride / 8 ? lane : kTabStride / 8 - 1;
         uint4 tv[kHufFrames];
 #pragma unroll
         for (int ff = 0; ff < kHufFrames; ff++) {
@@ -726,21 +712,23 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
         }
 #pragma unroll
         for (int ff = 0; ff < kHufFrames; ff++)
-            if (lane < (kTabStride < 504 ? kTabStride / 8 : 63)) *(uint4*)&tabs[ff * kTabStride + 8 * lane] = tv[ff];
+            if (lane < kTabStride / 8) *(uint4*)&tabs[ff * kTabStride + 8 * lane] = tv[ff];
         if (lane < kZeroTab / 2) ((uint32_t*)&tabs[kHufFrames * kTabStride])[lane] = 0u;
     }
     uint8_t* const junk = a.jobs + G * kStreams * kJobBytes + 128 * lane;
     Pp.mark(0);  // the job flags and the compact tables in LDS
     // this lane's stream
     uint64_t hp = 0, dstp = 0;
-    uint4 len = make_uint4(0, 0, 0, 0), prm = make_uint4(0, 11, 11, 0);
+    uint4 len = make_uint4(0, 0, 0, 0), prm = make_uint4(0, 11, 0, 0);
+    uint32_t C2 = 0;
     if (flag) {
         hp = gld<uint64_t>(&J->hp);
         dstp = gld<uint64_t>(&J->dst);
         len = gld<uint4>(&J->len[0]);
         prm = gld<uint4>(&J->rs);
+        C2 = gld<uint32_t>(&J->C2);
     }
-    const uint32_t rs = prm.x, tl = prm.y, K = prm.z, Cc = prm.w;
+    const uint32_t rs = prm.x, tl = prm.y, d1 = prm.z & 0xFFu, d2 = prm.z >> 8, C1 = prm.w;
     const uint32_t so = (q > 0 ? len.x : 0u) + (q > 1 ? len.y : 0u) + (q > 2 ? len.z : 0u);
     const uint32_t sl = sel4(len, q);
     const uint32_t seg = (rs + 3) / 4;
@@ -751,7 +739,7 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     bool bad = flag && lastB == 0;
     const bool live = flag && !bad;
     if (!live) nsym = 0;
-    const uint32_t sh1 = 32 - tl, sh2 = 32 - K;
+    const uint32_t sh1 = 32 - tl, shA = sh1 + d1, shB = sh1 + d2;
     // ---- bit reader.  Lanes without a stream read their junk line (readable, never decoded).
     const uint64_t e = live ? (uint64_t)src + sl - 1 : (uint64_t)junk;
     const uint64_t amin = live ? ((uint64_t)src & ~(uint64_t)15) : (uint64_t)junk;  // blocks holding stream bytes
@@ -831,20 +819,19 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
         insb += m01 << 8;
         nd = ring_at(insb);
     };
-    // table byte addresses: entry min(p, pq) of the lane's table, p = peek >> (32 - tl),
-    // pq = (peek >> (32 - K)) + Cc; tb / tc carry the table base (the zero table when frozen)
+    // table byte addresses: entry min(p, (p >> d1) + C1, (p >> d2) + C2) of the lane's compact table
+    // (pgn_hufjob.h), p = peek >> (32 - tl); tb / tc1 / tc2 carry the table base (the zero table when
+    // frozen: then every candidate is the zero table's base plus a peek shift, the smallest at most 15)
     const uint32_t tbLive = f * kTabStride, tbZero = kHufFrames * kTabStride;
-    uint32_t tb = tbLive, tc = Cc + tbLive, s1 = sh1;
+    uint32_t tb = tbLive, tc1 = C1 + tbLive, tc2 = C2 + tbLive, s1 = sh1;
     auto symbol = [&](bool merge) -> uint32_t {
         const uint32_t hi = (uint32_t)(C >> 32);
-        const uint32_t a1 = ((hi >> s1) + tb) << 1, a2 = ((hi >> sh2) + tc) << 1;
+        const uint32_t a0 = ((hi >> s1) + tb) << 1, a1 = ((hi >> shA) + tc1) << 1, a2 = ((hi >> shB) + tc2) << 1;
+        const uint32_t am = a0 < a1 ? a0 : a1;
 #if PGN_K2_DIAG == 3  // diagnostic (wrong output): the table read replaced by arithmetic on the peek
-        const uint32_t ent = ((a1 < a2 ? a1 : a2) & 0xFF00u) | (4u + (hi >> 30));
-#elif PGN_K2_DIAG == 4  // 256-entry tables: two more VALU per symbol
-        const uint32_t am = a1 < a2 ? a1 : a2;
-        const uint32_t ent = *(const uint16_t*)((const uint8_t*)tabs + (((am - 2 * tb) & 511u) + 2 * tb));
+        const uint32_t ent = ((am < a2 ? am : a2) & 0xFF00u) | (4u + (hi >> 30));
 #else
-        const uint32_t ent = *(const uint16_t*)((const uint8_t*)tabs + (a1 < a2 ? a1 : a2));
+        const uint32_t ent = *(const uint16_t*)((const uint8_t*)tabs + (am < a2 ? am : a2));
 #endif
         C = shl64(merge ? (C | Cadd) : C, ent);
         avail -= ent & 0xFFu;
@@ -862,7 +849,8 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     };
     auto freeze = [&](bool fz) {  // frozen: code length 0 from the zero table (peek < 16)
         tb = fz ? tbZero : tbLive;
-        tc = fz ? tbZero : Cc + tbLive;
+        tc1 = fz ? tbZero : C1 + tbLive;
+        tc2 = fz ? tbZero : C2 + tbLive;
         s1 = fz ? 28u : sh1;
     };
     // ---- output geometry: block D_m = output bytes [h + 16 m, h + 16 m + 16) at A0 + 16 m (16-byte

@@ -19,7 +19,7 @@ constexpr int kSeqHdr = 400;             // staged sequences-section header (tab
 constexpr int kSeqTab = 1280;            // LL [0,512) + OF [512,768) + ML [768,1280) FSE decode entries
 
 constexpr uint32_t kJobTab = 512;     // compact table slots of a deferred job (pgn_hufjob.h; 16-bit: nbBits | symbol << 8)
-constexpr uint32_t kJobTabUse = 504;  // entries a table may have: dec_huf_kernel keeps 504 per frame in LDS
+constexpr uint32_t kJobTabUse = 352;  // entries a job's compact table may have: dec_huf_kernel keeps 352 per frame in LDS
 constexpr unsigned kHufLdsLog = 11;  // Huffman tables up to this log live in LDS (zstd's encoders
                                      // never exceed 11); a 12-bit table is built in HBM (slow path)
 
@@ -337,6 +337,49 @@ __device__ __forceinline__ bool wdtable_build(HufBuildLds& H, const int16_t* nor
 // job's compact table, so the kernel needs no more LDS than H.
 // hw: when not null, the frame's header window (loaded at frame offset 0) and src at frame offset hoff:
 // the description is staged from it (lane-permute reads, no memory round trip) when it lies inside
+// A deferred job's compact table (pgn_hufjob.h), three segments.  T[d] = the table entries whose code
+// is longer than tl - d bits (weights <= d; rankStart[d + 1], T[0] = 0).  Entries [0, T1) stay whole,
+// [T1, T2) keep one entry per 2^d1 and [T2, 2^tl) one per 2^d2 (T1 = T[d1], T2 = T[d2]); the entry of
+// a peek p (the stream's next tl bits) is
+//     min(p, (p >> d1) + C1, (p >> d2) + C2),  C1 = T1 - (T1 >> d1),  C2 = T1 + ((T2 - T1) >> d1) - (T2 >> d2)
+// -- lines of slope 1, 2^-d1, 2^-d2 that cross at T1 and T2 (T[d] is a multiple of 2^d: the codes are
+// canonical and complete).  d1 = 0 is the two-segment table of round 4.  (d1, d2) are chosen for the
+// smallest table: on the bench's M / keys frames 300-345 / 190-240 entries, against 410-475 / 340-380
+// with two segments.
+struct JobSeg {
+    uint32_t d1, d2, T1, T2, C1, C2, size;
+};
+__device__ __forceinline__ JobSeg job_segments(const uint32_t (&T)[8], unsigned tl)
+{
+    const uint32_t tsz = 1u << tl;
+    JobSeg b{0, 0, 0, 0, 0, 0, tsz};
+    const uint32_t dmax = tl - 1 < 7u ? tl - 1 : 7u;
+#pragma unroll
+    for (uint32_t d1 = 0; d1 < 7; d1++) {
+#pragma unroll
+        for (uint32_t d2 = d1 + 1; d2 <= 7; d2++) {
+            if (d2 > dmax) continue;
+            const uint32_t t1 = T[d1], t2 = T[d2];
+            const uint32_t sz = t1 + ((t2 - t1) >> d1) + ((tsz - t2) >> d2);
+            if (sz < b.size) {
+                b.d1 = d1;
+                b.d2 = d2;
+                b.T1 = t1;
+                b.T2 = t2;
+                b.size = sz;
+            }
+        }
+    }
+    b.C1 = b.T1 - (b.T1 >> b.d1);
+    b.C2 = b.T1 + ((b.T2 - b.T1) >> b.d1) - (b.T2 >> b.d2);
+    return b;
+}
+// compact entry j -> its index in the full 2^tl-entry table
+__device__ __forceinline__ uint32_t job_entry_index(const JobSeg& g, uint32_t j)
+{
+    return j < g.T1 ? j : (j < g.T1 + ((g.T2 - g.T1) >> g.d1) ? (j - g.C1) << g.d1 : (j - g.C2) << g.d2);
+}
+
 template <bool JobOnly = false>
 __device__ __forceinline__ size_t huf_build_dtable_body(HufBuildLds& H, const uint8_t* src, size_t srcSize, unsigned* tlOut, uint16_t* gt,
                                                        unsigned* minNbOut, const HdrWin* hw = nullptr, uint32_t hoff = 0,
@@ -518,22 +561,13 @@ __device__ __forceinline__ size_t huf_build_dtable_body(HufBuildLds& H, const ui
         // first rankStart[d + 1] of the table; entry idx belongs to the last weight whose range starts
         // at or below it.  A table above kJobTabUse entries returns 0: the caller's general path.
         if (tl > kHufLdsLog) return 0;
-        const uint32_t tsz = 1u << tl;
-        uint32_t K = tl, T = 0, size = tsz;
+        uint32_t Td[8];
 #pragma unroll
-        for (uint32_t d = 1; d <= 4; d++) {
-            if (d >= tl) break;
-            const uint32_t t = rankStart[d + 1], sz = t + ((tsz - t) >> d);
-            if (sz < size) {
-                size = sz;
-                K = tl - d;
-                T = t;
-            }
-        }
-        if (size > kJobTabUse) return 0;
-        const uint32_t d = tl - K, Cc = T - (T >> d);
-        for (uint32_t j = (uint32_t)lane; j < size; j += 64) {
-            const uint32_t idx = j < T ? j : (j - Cc) << d;
+        for (int d = 0; d < 8; d++) Td[d] = rankStart[d + 1];
+        const JobSeg sg = job_segments(Td, tl);
+        if (sg.size > kJobTabUse) return 0;
+        for (uint32_t j = (uint32_t)lane; j < sg.size; j += 64) {
+            const uint32_t idx = job_entry_index(sg, j);
             uint32_t w = 0, rs0 = 0, bf = 0;
 #pragma unroll
             for (unsigned ww = 1; ww <= 12; ww++) {
@@ -545,8 +579,9 @@ __device__ __forceinline__ size_t huf_build_dtable_body(HufBuildLds& H, const ui
             const uint32_t sym = H.order[bf + ((idx - rs0) >> (w - 1))];
             gst<uint16_t>(jobTab + 2 * j, (uint16_t)((tl + 1 - w) | (sym << 8)));
         }
-        jobKC[0] = K;
-        jobKC[1] = Cc;
+        jobKC[0] = sg.d1 | (sg.d2 << 8);
+        jobKC[1] = sg.C1;
+        jobKC[2] = sg.C2;
         *tlOut = tl;
         uint32_t wmx = 0;
 #pragma unroll
@@ -1370,7 +1405,7 @@ __device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, 
     if (hw_byte(hw, src, ip + lh + cs) != 0) return -1;  // the sequences section: none
     const uint8_t* hp = src + ip + lh;
     unsigned tl = 0, mn = 1;
-    uint32_t kc[2] = {0, 0};
+    uint32_t kc[3] = {0, 0, 0};
     const size_t hsz = huf_build_dtable_body<true>(H, hp, cs, &tl, htab, &mn, &hw, (uint32_t)(ip + lh), &P, job + sizeof(HufJob), kc);
     P.mark(1);
     if (hsz == 0 || tl > kHufLdsLog || cs - hsz < 6) return -1;
@@ -1379,7 +1414,7 @@ __device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, 
     const size_t jp = (size_t)(hp - src);
     const uint32_t jt01 = hw_u16(hw, src, jp) | (hw_u16(hw, src, jp + 2) << 16);
     const uint32_t jt2 = hw_u16(hw, src, jp + 4);
-    if (!huf_defer_header(job, tl, hp, remain, dst, (uint32_t)rs, jt01, jt2, kc[0], kc[1])) return -1;
+    if (!huf_defer_header(job, tl, hp, remain, dst, (uint32_t)rs, jt01, jt2, kc)) return -1;
     return (long)rs;
 }
 
