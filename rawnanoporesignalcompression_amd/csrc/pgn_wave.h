@@ -161,6 +161,15 @@ __device__ __forceinline__ void gst<uint4>(void* p, uint4 v)
     ((PGN_GLOBAL Unal<pgn_u32x4>*)p)->v = t;
 }
 
+// Non-temporal 16-byte store (the nt bit: data written once is not kept in the caches at the expense
+// of data that is reused); 16-byte aligned addresses only.
+__device__ __forceinline__ void gst_nt16(void* p, uint4 v)
+{
+    pgn_u32x4 t;
+    t.x = v.x; t.y = v.y; t.z = v.z; t.w = v.w;
+    __builtin_nontemporal_store(t, (PGN_GLOBAL pgn_u32x4*)p);
+}
+
 // unaligned little-endian loads (gfx950 global memory accepts unaligned dword accesses)
 __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) { return gld<uint32_t>(p); }
 __device__ __forceinline__ uint64_t ld64u(const uint8_t* p) { return gld<uint64_t>(p); }
