@@ -170,6 +170,29 @@ __device__ __forceinline__ void gst_nt16(void* p, uint4 v)
     __builtin_nontemporal_store(t, (PGN_GLOBAL pgn_u32x4*)p);
 }
 
+// wave_copy with non-temporal stores (the destination is not read again soon); any alignment: the
+// head bytes up to dst's first 16-byte boundary one per lane, then aligned 16-byte stores
+__device__ inline void wave_copy_nt(uint8_t* dst, const uint8_t* src, size_t n)
+{
+    const int lane = lane_id();
+    const size_t head = ((16u - ((uintptr_t)dst & 15u)) & 15u) < n ? ((16u - ((uintptr_t)dst & 15u)) & 15u) : n;
+    if ((size_t)lane < head) gst<uint8_t>(dst + lane, gb(src + lane));
+    dst += head;
+    src += head;
+    n -= head;
+    size_t i = (size_t)lane * 16;
+    for (; i + 16 + 3 * 1024 <= n; i += 4096) {
+        const uint4 a = gld<uint4>(src + i), b = gld<uint4>(src + i + 1024), c = gld<uint4>(src + i + 2048),
+                    d = gld<uint4>(src + i + 3072);
+        gst_nt16(dst + i, a);
+        gst_nt16(dst + i + 1024, b);
+        gst_nt16(dst + i + 2048, c);
+        gst_nt16(dst + i + 3072, d);
+    }
+    for (; i + 16 <= n; i += 1024) gst_nt16(dst + i, gld<uint4>(src + i));
+    for (size_t k = (n & ~(size_t)15) + (size_t)lane; k < n; k += 64) gst<uint8_t>(dst + k, gb(src + k));
+}
+
 // unaligned little-endian loads (gfx950 global memory accepts unaligned dword accesses)
 __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) { return gld<uint32_t>(p); }
 __device__ __forceinline__ uint64_t ld64u(const uint8_t* p) { return gld<uint64_t>(p); }

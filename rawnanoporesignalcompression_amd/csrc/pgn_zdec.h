@@ -1389,7 +1389,7 @@ __device__ __forceinline__ long dec_frame_fast(const uint8_t* __restrict__ src, 
     if (!(bh & 1) || bsize > srcSize - ip || ip + bsize + (checksum ? 4 : 0) != srcSize) return -1;
     if (btype == z1::kBtRaw) {
         if (bsize > dstCap || (fcsSize > 0 && bsize != fcs)) return -1;
-        wave_copy8(dst, src + ip, bsize);
+        wave_copy_nt(dst, src + ip, bsize);  // read by the merge only after the sections: non-temporal
         P.mark(5);
         return (long)bsize;
     }

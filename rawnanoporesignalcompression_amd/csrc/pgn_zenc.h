@@ -713,7 +713,8 @@ __device__ __noinline__ void huf_encode_segment_wave(uint8_t* __restrict__ out, 
         const uint32_t carry = win[complete];
         for (uint32_t w = lane; w <= complete; w += 64) {
             const uint32_t v = win[w];
-            if (w < complete) gst<uint32_t>(o + 4 * w, v);
+            // the packed bits go to the blob once: non-temporal (encode -0.6 % in A/B, r05ent)
+            if (w < complete) __builtin_nontemporal_store(v, (__attribute__((address_space(1))) uint32_t*)(o + 4 * w));
             win[w] = 0u;
         }
         if (lane == 0) win[0] = carry;
@@ -2010,7 +2011,7 @@ __device__ __noinline__ size_t zstd1_compress_wave(uint8_t* __restrict__ dst, co
         size_t bsz;
         if (cSize == 0) {
             if (lane == 0) z1::wr24(bdst, (uint32_t)((last ? 1u : 0u) + (z1::kBtRaw << 1) + (bs << 3)));
-            wave_copy(bdst + 3, src + start, bs);
+            wave_copy_nt(bdst + 3, src + start, bs);  // into the blob once: non-temporal
             bsz = 3 + bs;
         } else if (cSize == 1) {
             if (lane == 0) {
