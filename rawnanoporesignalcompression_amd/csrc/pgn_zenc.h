@@ -97,6 +97,7 @@ __device__ __forceinline__ uint32_t seg_count(const EncLds& L, int k, int s)
 
 // One instance per encode workgroup (the shared codec LDS, pgn_wave.h: every access is a DS instruction).
 static_assert(sizeof(EncLds) <= kCodecLdsBytes, "encoder LDS exceeds the codec LDS");
+static_assert(__builtin_offsetof(EncLds, hdr) % 4 == 0, "table description words");
 #define sEnc (*reinterpret_cast<EncLds*>(sCodecLds))
 
 struct EncScratch {
@@ -1218,30 +1219,21 @@ __device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t
                 const size_t nh = z1::fse_write_ncount(L.hdr + 1, L.wnorm, maxW, tableLog);
                 if (nh && wtSize > 2) {
                     fse_build_ctable_small(L.fct, L.wnorm, maxW, tableLog, L.fscratch, L.wcumul);
-                    // FSE_compress_usingCTable (two interleaved states), wave-uniform over registers:
-                    // table entry u / symbol s in lane u / s (read with v_readlane), weight of symbol
-                    // i in lane i & 63 of w[i >> 6]; the bitstream collects as 32-bit words in lane
-                    // order (<= 255 * 6 bits).
+                    // FSE_compress_usingCTable (two interleaved states) in two passes.  The states run
+                    // serially and wave-uniform (table entry u / symbol s in lane u / s, read with
+                    // v_readlane): chain X starts from the last weight, chain Y from the one before, and
+                    // emission k (k = 0 .. n - 3) encodes weight n - 3 - k on chain X (k even) or Y (k
+                    // odd); each emission only records its state and bit count into lane k & 63 of
+                    // rec[k >> 6] (the reference's bit-container flushes do not change the bit order).
+                    // Then the fields' offsets come from a wave prefix sum and their bits are ORed into
+                    // the description in LDS, so the serial loop carries no bit packing (it was ~26
+                    // scalar instructions per weight).
                     const uint32_t vST = ((uint32_t)lane < (1u << tableLog)) ? (uint32_t)L.fct.stateTable[lane] : 0u;
                     const uint32_t vDN = ((uint32_t)lane <= maxW) ? L.fct.deltaNbBits[lane] : 0u;
                     const uint32_t vDF = ((uint32_t)lane <= maxW) ? (uint32_t)L.fct.deltaFindState[lane] : 0u;
-                    // weight of symbol i: byte i & 3 of lane i >> 2 of W4 (one readlane and a scalar bit-field
-                    // extract: selecting among w[0..3] by i >> 6 compiled to a chain of scalar branches per symbol)
                     const uint32_t W4 = reinterpret_cast<const uint32_t*>(L.weights)[lane];
                     auto wsym = [&](uint32_t i) -> uint32_t {
                         return (readlane_u32(W4, (int)(i >> 2)) >> (8u * (i & 3u))) & 0xFFu;
-                    };
-                    uint32_t wv = 0, nw = 0, nacc = 0;
-                    uint64_t acc = 0;
-                    auto put = [&](uint32_t v, uint32_t nb) {  // nb <= 7
-                        acc |= (uint64_t)(v & ((1u << nb) - 1u)) << nacc;
-                        nacc += nb;
-                        if (nacc >= 32) {
-                            wv = ((uint32_t)lane == nw) ? (uint32_t)acc : wv;
-                            nw++;
-                            acc >>= 32;
-                            nacc -= 32;
-                        }
                     };
                     auto init = [&](uint32_t sym) -> uint32_t {
                         const uint32_t dn = readlane_u32(vDN, (int)sym), df = readlane_u32(vDF, (int)sym);
@@ -1249,47 +1241,66 @@ __device__ __noinline__ uint32_t huf_write_ctable_wave(uint32_t maxSym, uint32_t
                         const uint32_t v = (nbo << 16) - dn;
                         return readlane_u32(vST, (int)((v >> nbo) + df));
                     };
-                    auto enc = [&](uint32_t& st, uint32_t sym) {
-                        const uint32_t dn = readlane_u32(vDN, (int)sym), df = readlane_u32(vDF, (int)sym);
+                    const uint32_t n = wtSize, nEm = n - 2;
+                    // each emission's deltas, lane-parallel
+                    uint32_t dnR[4], dfR[4], rec[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t k = (uint32_t)lane + 64u * (uint32_t)r;
+                        const uint32_t sy = k < nEm ? (uint32_t)L.weights[n - 3 - k] : 0u;
+                        dnR[r] = L.fct.deltaNbBits[sy];
+                        dfR[r] = (uint32_t)L.fct.deltaFindState[sy];
+                        rec[r] = 0;
+                    }
+                    uint32_t stX = init(wsym(n - 1)), stY = init(wsym(n - 2));
+                    auto enc = [&](uint32_t& st, uint32_t& rc, uint32_t dv, uint32_t fv, uint32_t k) {
+                        const uint32_t dn = readlane_u32(dv, (int)(k & 63u)), df = readlane_u32(fv, (int)(k & 63u));
                         const uint32_t nbo = (st + dn) >> 16;
-                        put(st, nbo);
+                        // (one SGPR read per VALU instruction on gfx950: the lane select goes through m0)
+                        asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(rc) : "s"(st | (nbo << 16)), "{m0}"(k & 63u));
                         st = readlane_u32(vST, (int)((st >> nbo) + df));
                     };
-                    uint32_t ip = wtSize;
-                    uint32_t s1, s2;
-                    if (wtSize & 1) {
-                        s1 = init(wsym(ip - 1));
-                        s2 = init(wsym(ip - 2));
-                        enc(s1, wsym(ip - 3));
-                        ip -= 3;
-                    } else {
-                        s2 = init(wsym(ip - 1));
-                        s1 = init(wsym(ip - 2));
-                        ip -= 2;
-                    }
-                    if ((wtSize - 2) & 2) {
-                        enc(s2, wsym(ip - 1));
-                        enc(s1, wsym(ip - 2));
-                        ip -= 2;
-                    }
-                    while (ip > 0) {
-                        enc(s2, wsym(ip - 1));
-                        enc(s1, wsym(ip - 2));
-                        enc(s2, wsym(ip - 3));
-                        enc(s1, wsym(ip - 4));
-                        ip -= 4;
-                    }
-                    put(s2, tableLog);
-                    put(s1, tableLog);
-                    put(1, 1);  // end mark
-                    const uint32_t tailBytes = (nacc + 7) >> 3;
-                    uint8_t* op = L.hdr + 1 + nh;
-                    if ((uint32_t)lane < nw) {
 #pragma unroll
-                        for (int b = 0; b < 4; b++) op[4 * lane + b] = (uint8_t)(wv >> (8 * b));
+                    for (uint32_t r = 0; r < 4; r++) {
+                        const uint32_t kEnd = nEm < 64u * r + 64u ? nEm : 64u * r + 64u;
+                        for (uint32_t k = 64u * r; k < kEnd; k += 2) {  // a pair never crosses a register
+                            enc(stX, rec[r], dnR[r], dfR[r], k);
+                            if (k + 1 < kEnd) enc(stY, rec[r], dnR[r], dfR[r], k + 1);
+                        }
                     }
-                    if ((uint32_t)lane < tailBytes) op[4 * nw + lane] = (uint8_t)(acc >> (8 * lane));
-                    hSize = (uint32_t)(nh + 4 * nw + tailBytes);
+                    // FSE_flushCState of the second state, then the first (even n: X then Y; odd n: Y
+                    // then X), then the end mark
+                    const uint32_t fA = ((n & 1u) ? stY : stX) | (tableLog << 16), fB = ((n & 1u) ? stX : stY) | (tableLog << 16);
+                    uint32_t pos[4], tot = 0;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t k = (uint32_t)lane + 64u * (uint32_t)r;
+                        if (k == nEm) rec[r] = fA;
+                        if (k == nEm + 1) rec[r] = fB;
+                        if (k == nEm + 2) rec[r] = 1u | (1u << 16);
+                        const uint32_t nb = k < nEm + 3 ? rec[r] >> 16 : 0u;
+                        const uint32_t incl = wave_incl_sum(nb);
+                        pos[r] = tot + incl - nb;
+                        tot += readlane_u32(incl, 63);
+                    }
+                    const uint32_t bytes = (tot + 7) >> 3;
+                    uint8_t* op = L.hdr + 1 + nh;
+                    for (uint32_t b = (uint32_t)lane; b < bytes; b += 64) op[b] = 0;
+                    lds_sync();
+                    lds_u32* hw = (lds_u32*)(uint32_t*)L.hdr;  // 4-byte aligned (static_assert below)
+                    const uint32_t B0 = 8u * (1u + (uint32_t)nh);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const uint32_t k = (uint32_t)lane + 64u * (uint32_t)r;
+                        if (k < nEm + 3) {
+                            const uint32_t nb = rec[r] >> 16, v = rec[r] & ((1u << nb) - 1u);
+                            const uint32_t P = B0 + pos[r], w = P >> 5, sh = P & 31u;
+                            __hip_atomic_fetch_or(&hw[w], v << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                            if (sh + nb > 32u)
+                                __hip_atomic_fetch_or(&hw[w + 1], v >> (32u - sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                        }
+                    }
+                    hSize = (uint32_t)(nh + bytes);
                 }
             }
         }
