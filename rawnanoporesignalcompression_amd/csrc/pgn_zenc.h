@@ -881,9 +881,11 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
             if (j < leafSlots) {
                 const uint32_t i = (uint32_t)lane + 64u * (uint32_t)j;
                 uint32_t lo = 0;
+                // branch-free: a probe past the run is clamped to its last element (the predicate is
+                // monotone, so taking the clamped position when it holds is still exact)
                 for (uint32_t st = stN; st; st >>= 1) {
-                    const uint32_t k = lo + st;
-                    if (k <= nq && hn[lowN + (int)k - 1].count <= lv[j]) lo = k;
+                    const uint32_t k = lo + st, kc = k < nq ? k : nq;
+                    lo = hn[lowN + (int)kc - 1].count <= lv[j] ? kc : lo;
                 }
                 const uint32_t pos = i + lo;
                 const bool take = i < nl && pos < used;
@@ -903,8 +905,8 @@ __device__ __noinline__ uint32_t huf_tree_wave(uint32_t maxSym, uint32_t maxNbBi
                     const uint32_t v = hn[lowN + (int)m].count;
                     uint32_t lo = 0;
                     for (uint32_t st = stL; st; st >>= 1) {
-                        const uint32_t k = lo + st;
-                        if (k <= nl && hn[lowS - (int)k + 1].count < v) lo = k;
+                        const uint32_t k = lo + st, kc = k < nl ? k : nl;
+                        lo = hn[lowS - (int)kc + 1].count < v ? kc : lo;
                     }
                     const uint32_t pos = m + lo;
                     if (pos < used) {
