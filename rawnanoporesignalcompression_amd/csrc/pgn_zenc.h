@@ -9,7 +9,7 @@
 // Serial stages (tree build, weight FSE, sequence FSE) run on lane 0 with the shared zstd1_* code.
 #pragma once
 #ifndef PGN_AB_SKIP
-#define PGN_AB_SKIP 0  // diagnostic builds (tools/ab_skip.sh): 1 no zstd stage, 2 search only, 3 no Huffman, 4 no bit packing;
+#define PGN_AB_SKIP 0  // diagnostic builds (tools/ab_skip.sh): 1 no zstd stage, 2 search only, 3 no Huffman, 4 no bit packing, 5 tree only;
                        // PGN_AB_HLOG=h caps the hash log (table-footprint probe)
 #endif
 #include "pgn_c5.h"
@@ -1789,6 +1789,9 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
     for (int q = 0; q < 4; q++) nnz += (uint32_t)__builtin_popcountll(ballot(c[q] != 0));
     const uint32_t hl = huf_tree_wave(maxSym, huffLog, nnz, P);
     P.mark(14);
+#if PGN_AB_SKIP == 5  // diagnostic: stop after the tree (instruction attribution of the table description)
+    { size_t r = write_raw_literals_wave(dst, lit, n); return ret(r + 0 * hl, false); }
+#endif
     if (!repeat) {
         // the streams alone already miss the gain the section must make: raw literals whatever the
         // table description's size (HUF_compress_internal's final check), so it is not written
