@@ -1645,7 +1645,11 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
         hist_segment_wave(lit, n, segSize, 0);
         __syncthreads();  // B2
     }
-    // per-segment histograms; the 16-byte loads of four 1024-byte steps are issued together
+    // per-segment histograms; the 16-byte loads of four 1024-byte steps are issued together.  A
+    // block's segment i / segSize is one multiply-high by ceil(2^32 / segSize): exact here because
+    // i < 2^17 (a block is at most 128 KiB) and segSize <= 2^15, so i times the reciprocal's error
+    // stays below 2^32 (the general division took ~15 instructions per block)
+    const uint32_t segMagic = 0xFFFFFFFFu / segSize + 1u;
     for (uint32_t i0 = (uint32_t)lane * 16; i0 < ((COOP && !single) ? 0u : n); i0 += 4096) {
         uint4 v[4];
 #pragma unroll
@@ -1664,7 +1668,7 @@ __device__ __noinline__ LitOut compress_literals_wave(uint8_t* __restrict__ dst,
         for (int u = 0; u < 4; u++) {
             const uint32_t i = i0 + 1024u * (uint32_t)u;
             const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-            const uint32_t sa = i / segSize;
+            const uint32_t sa = __umulhi(i, segMagic);
             const uint32_t boundary = (sa + 1) * segSize;
             if (i + 16 <= n && i + 16 <= boundary) {  // the usual case: 16 bytes of one segment
                 uint32_t* h = ((lane & 1) ? &L.hist2x[1] : &L.hist2[0][0]) + 256 * (sa >> 1);
