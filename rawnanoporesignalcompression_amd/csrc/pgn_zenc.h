@@ -118,23 +118,24 @@ struct EncScratch {
 // ---------------------------------------------------------------------------------------------
 __device__ inline uint32_t wave_match_count(const uint8_t* src, uint32_t a, uint32_t b, uint32_t end)
 {
-    const int lane = lane_id();
+    // 256 bytes per round, four per lane from one unaligned dword load per side (both in flight
+    // together: one memory round trip per round; the byte-wise compare with an early exit made four
+    // dependent ones).  At the end the lane's dword is taken from end - 4 (or earlier) and shifted, so no
+    // byte past `end` is compared; the bytes loaded before a + n lie inside the stream's buffer.
+    const uint32_t o = 4u * (uint32_t)lane_id();
     uint32_t n = 0;
     while (a + n < end) {
-        uint32_t len = end - (a + n);
-        uint32_t mism = 0xFFFFFFFFu;  // first mismatching offset within this lane's 4 bytes
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            uint32_t o = 4u * (uint32_t)lane + (uint32_t)j;
-            if (o < len && mism == 0xFFFFFFFFu && gb(src + a + n + o) != gb(src + b + n + o)) mism = o;
-        }
-        bool over = (4u * (uint32_t)lane + 4u > len);
-        uint64_t mm = ballot(mism != 0xFFFFFFFFu);
-        if (mm) {
-            int f = __builtin_ctzll(mm);
-            return n + readlane_u32(mism, f);
-        }
-        if (ballot(over)) return len + n;  // matched to the end
+        const uint32_t len = end - (a + n);
+        const uint32_t nv = len > o ? (len - o < 4u ? len - o : 4u) : 0u;  // my bytes inside the stream
+        const int32_t so = (int32_t)len - 4 < (int32_t)o ? (int32_t)len - 4 : (int32_t)o;
+        const uint32_t wa = ld32u(src + (int64_t)(a + n) + so), wb = ld32u(src + (int64_t)(b + n) + so);
+        const uint32_t sh = 8u * (uint32_t)((int32_t)o - so);  // 0, or up to 24 for the end lane
+        uint32_t x = nv ? ((wa ^ wb) >> sh) : 0u;
+        x &= nv >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nv)) - 1u);
+        const uint32_t mism = x ? o + ((uint32_t)__builtin_ctz(x) >> 3) : 0xFFFFFFFFu;
+        const uint64_t mm = ballot(mism != 0xFFFFFFFFu);
+        if (mm) return n + readlane_u32(mism, __builtin_ctzll(mm));
+        if (len <= 256u) return len + n;  // matched to the end
         n += 256;
     }
     return n;
