@@ -345,6 +345,50 @@ def per_chunk_plugin(torch, codec, S, seed, nreads=200):
             "sample": f"{nreads} reads x {S} samples, one pgn_compress_signal / pgn_decompress_signal call each"}
 
 
+def per_chunk_plugin_threads(torch, codec, S, seed, nthreads=16, nreads=1600):
+    """The per-chunk surface under concurrent callers on one context (the reference's reader calls
+    it from the async signal loader's worker threads, async_signal_loader.cpp:174-208): nthreads
+    host threads, each one chunk per call; calls that meet on the device are combined into one
+    small batch (pgn_kernels.hip PcArena)."""
+    import threading
+
+    samples, offs, counts = codec.synth_reads(nreads, S, seed=seed)
+    host = samples.cpu().numpy()
+    torch.cuda.synchronize()
+    xs = [host[r * S:(r + 1) * S] for r in range(nreads)]
+    blobs = [None] * nreads
+    ok = [True]
+
+    def run(fn):
+        def work(i):
+            for r in range(i, nreads, nthreads):
+                fn(r)
+        ts = [threading.Thread(target=work, args=(i,)) for i in range(nthreads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        return time.perf_counter() - t0
+
+    def enc(r):
+        blobs[r] = codec.compress_signal(xs[r])
+
+    def dec(r):
+        y = codec.decompress_signal(blobs[r], sample_count=S)
+        if r % 97 == 0 and not (y == xs[r]).all():
+            ok[0] = False
+
+    run(lambda r: enc(r) if r < 2 * nthreads else None)  # warm the arenas
+    te = run(enc)
+    td = run(dec)
+    n = nreads * S
+    return {"encode_msamples_s": round(n / te / 1e6, 1), "decode_msamples_s": round(n / td / 1e6, 1),
+            "threads": nthreads, "round_trip_ok": ok[0],
+            "sample": f"{nreads} reads x {S} samples over {nthreads} host threads on one context, "
+                      "one pgn_compress_signal / pgn_decompress_signal call each"}
+
+
 def pod5_batch_host(torch, codec, S, seed, nreads=1000):
     """The batched POD5 integration (include/pgnano_pod5.h) on host memory: one
     pod5_add_reads_data-shaped call (reads chunked at the writer's 102,400 samples, all chunks in one
@@ -630,6 +674,7 @@ def main(argv=None):
         side["stream_copy_gbs"] = round(stream_copy_gbs(torch), 1)
         side["pcie_inclusive"] = pcie_inclusive(torch, codec, args.samples, args.seed)
         side["per_chunk_plugin"] = per_chunk_plugin(torch, codec, args.samples, args.seed)
+        side["per_chunk_plugin_threads"] = per_chunk_plugin_threads(torch, codec, args.samples, args.seed)
         side["pod5_batch_host"] = pod5_batch_host(torch, codec, args.samples, args.seed)
     line = run_rank(args, rank, world, local, codec, torch, dist, device=torch.device("cuda", dev_index))
     if line is not None:

@@ -9,6 +9,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <condition_variable>
 #include <mutex>
 
 #include "../../include/pgnano_hip.h"
@@ -502,6 +504,7 @@ struct DecArgs {
     uint64_t epoch;      // this call's tag in those words (bits 48..63)
     uint32_t coopParse;  // dec_zstd_coop_kernel parses the chunks itself (no dec_parse_kernel launch)
     uint8_t* jobs;       // [G][5] HufJob records (pgn_hufjob.h): dec_zstd_kernel defers, dec_huf_kernel decodes; null = in place
+    uint32_t hufPrio;    // dec_huf_kernel waves at raised priority (the last deferred pass: the decode's drain)
 };
 
 // The status of a chunk whose frames claim more content (ZSTD_getFrameContentSize) than the
@@ -695,6 +698,7 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     const uint32_t flag = inb ? gld<uint32_t>(&J->flag) : 0u;
     const uint64_t fm = ballot(flag != 0);
     if (fm == 0) return;
+    if (a.hufPrio) __builtin_amdgcn_s_setprio(3);  // ahead of the merges sharing the CU (the drain)
     // phase profile build: dec_huf's own region of the profile buffer (kHufProfOff, DecArgs.prof = +kPhases)
     PhaseProf Pp;
     Pp.init(a.prof ? a.prof + (kHufProfOff - kPhases) : nullptr);
@@ -1752,6 +1756,42 @@ __global__ void large_scan_kernel(const uint32_t* counts, size_t n, uint32_t* li
 // =============================================================================================
 using namespace pgn;
 
+// ---- concurrent per-chunk host calls ------------------------------------------------------------
+// The reference's readers call the plugin surface from several threads at once (the pod5 async
+// signal loader's workers, async_signal_loader.cpp:174-208 -> signal_table_reader.cpp:135-139).  Calls
+// on one context that arrive while another is on the device are combined into one small batch
+// (flat combining): each call reserves room in the open arena (pinned host memory with a device
+// mirror), copies its input there itself, and the first caller that finds the device free runs the
+// whole arena as one batch -- one upload, the small-batch kernels for up to kPcMaxReqs chunks, one
+// wait -- while later callers fill the other arena.  Each caller copies its own result out.
+constexpr int kPcMaxReqs = 64;                    // the small-batch kernels' batch limit
+constexpr size_t kPcHdr = 16384;                  // per-request arrays (<= 136 B per request)
+constexpr size_t kPcInCap = (size_t)32 << 20;     // input bytes of one arena
+constexpr size_t kPcOutCap = (size_t)32 << 20;    // output bytes of one arena
+struct PcReq {
+    int dir;             // 0 encode, 1 decode
+    int codec;
+    const void* in;      // samples (encode) or blob (decode), caller's host memory
+    size_t inBytes;
+    uint32_t n;          // samples
+    void* dst;           // encode: blob destination; decode: samples
+    size_t cap;          // encode: the destination's capacity
+    size_t outBytes;     // room reserved for the result
+    size_t inOff, outOff;
+    int rc;
+    uint64_t outSize;    // encode: blob size (or the required size on PGN_ERR_DST_TOO_SMALL)
+    bool done;
+};
+struct PcArena {
+    uint8_t* h = nullptr;     // pinned: [arrays | inputs | outputs]
+    uint8_t* hDev = nullptr;  // the device's address of h (the kernels write results there)
+    uint8_t* d = nullptr;     // device mirror of [arrays | inputs]
+    size_t inUsed = 0, outUsed = 0;
+    PcReq* reqs[kPcMaxReqs] = {};
+    int nreq = 0, unstaged = 0, readers = 0;
+    int state = 0;            // 0 idle / open, 1 on the device, 2 results being copied out
+};
+
 struct pgn_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1773,6 +1813,12 @@ struct pgn_ctx {
     // needs thousands of frames in flight (PGN_DEFER_MIN_CHUNKS / PGN_DEFER_G tune both; the output
     // is the same either way)
     size_t deferMin = 12288, deferG = 12500;
+    // the last pass of a deferred call decodes its Huffman sections in place (dec_zstd_kernel's 16-
+    // lanes-per-stream decoder): this many chunks (PGN_DEFER_TAIL_PLAIN; 0 = every pass deferred).
+    // A deferred pass ends with one lane's ~16,000-symbol chain per M stream, which nothing overlaps
+    // once the frame decode of the last pass is done (the decode's drain)
+    size_t deferTailPlain = 0;
+    bool hufPrioLast = false;  // PGN_HUF_PRIO_LAST=1: the last deferred pass's dec_huf waves at raised priority
     bool lastDeferred = false;  // the last staged C5 decode deferred its Huffman sections (pgn_ctx_kernels)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
@@ -1845,6 +1891,13 @@ struct pgn_ctx {
     uint8_t* largeDecScratch = nullptr;
     size_t largeDecScratchBytes = 0;
     std::mutex mu;
+    // combined per-chunk host calls (PcArena): pcOpen = the arena new calls join (-1: none idle)
+    std::mutex pcMu;
+    std::condition_variable pcCv;
+    PcArena pcA[2];
+    int pcOpen = 0;
+    bool pcBusy = false;
+    int pcReady = 0;  // 0 not yet allocated, 1 ready, -1 allocation failed (calls run one by one)
 };
 
 static thread_local char g_err[512];
@@ -1935,6 +1988,8 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     }
     if (const char* v = getenv("PGN_DEFER_MIN_CHUNKS")) { const long x = atol(v); if (x > 0) c->deferMin = (size_t)x; }
     if (const char* v = getenv("PGN_DEFER_G")) { const long x = atol(v); if (x > 0) c->deferG = (size_t)x; }
+    if (const char* v = getenv("PGN_HUF_PRIO_LAST")) c->hufPrioLast = v[0] == '1';
+    if (const char* v = getenv("PGN_DEFER_TAIL_PLAIN")) { const long x = atol(v); if (x >= 0) c->deferTailPlain = (size_t)x; }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     const char* pe = getenv("PGN_PHASE_PROFILE");
     if (pe && pe[0] == '1') {
@@ -1999,6 +2054,10 @@ int pgn_ctx_destroy(pgn_ctx* c)
     (void)hipFree(c->stage);
     if (c->hstage) (void)hipHostFree(c->hstage);
     (void)hipFree(c->prof);
+    for (PcArena& A : c->pcA) {
+        if (A.h) (void)hipHostFree(A.h);
+        (void)hipFree(A.d);
+    }
     if (c->scanStream) (void)hipStreamSynchronize(c->scanStream);
     (void)hipFree(c->largeList);
     (void)hipFree(c->largeHdr);
@@ -2330,18 +2389,28 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     // balanced over the batch; otherwise passes of subBatch chunks
     bool defer = codec == kCodecC5 && nchunks >= c->deferMin;
     const size_t stride = chunk_inter_bytes(capCall);
-    size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;
+    size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;  // chunks per pass (the buffers' capacity)
+    size_t Gd = G, nDef = nchunks;  // deferred calls: Gd chunks per deferred pass over the first nDef chunks
     if (defer) {  // up to deferG chunks per pass, and decBufs passes' buffers within kDecBufferBudget
+        // (the budget's bound is at least subBatch chunks; PGN_DEFER_G below that is the tests' way to
+        // run several passes on small batches)
         size_t gmax = kDecBufferBudget / (c->decBufs * (stride + kStreams * (sizeof(DecUnit) + kJobBytes)));
-        gmax = gmax < c->deferG ? gmax : c->deferG;
         gmax = gmax < c->subBatch ? c->subBatch : gmax;
-        const size_t np = (nchunks + gmax - 1) / gmax;
-        G = (nchunks + np - 1) / np;
+        gmax = gmax < c->deferG ? gmax : c->deferG;
+        // the last deferTailPlain chunks: one pass whose sections are decoded in place (no drain of
+        // lane-per-stream chains after the last frame decode)
+        const size_t tail = c->deferTailPlain;
+        if (tail > 0 && tail <= gmax && nchunks >= 2 * tail) nDef = nchunks - tail;
+        const size_t np = (nDef + gmax - 1) / gmax;
+        Gd = (nDef + np - 1) / np;
+        const size_t tailN = nchunks - nDef;
+        G = Gd > tailN ? Gd : tailN;
     }
-    const size_t passes = (nchunks + G - 1) / G;
+    const size_t passes = defer ? (nDef + Gd - 1) / Gd + (nDef < nchunks ? 1 : 0) : (nchunks + G - 1) / G;
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
     const size_t slots = nu * G < c->decSlotsMax ? nu * G : c->decSlotsMax;
-    const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots;  // few chunks: a workgroup per frame
+    // few chunks: a workgroup per frame (not for the passes of a larger deferred call)
+    const bool coop = G <= kCoopMaxChunks && (size_t)nu * G <= slots && !(defer && nchunks > kCoopMaxChunks);
     defer = defer && !coop;  // the cooperative kernel decodes its sections itself
     c->lastDeferred = defer;
     // buffers in rotation: a pass parses into buffer p % nbuf once the merge of pass p - nbuf has read it
@@ -2399,12 +2468,18 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     for (size_t p = 0; p < passes; p++) {
         const int b = (int)(p % nbuf);
         uint8_t* buf = c->decChunks + (size_t)b * bufBytes;
+        // this pass: chunks [base, base + a.G); a deferred call's last pass may be its in-place tail
+        const bool tailPass = defer && p * Gd >= nDef;
+        const bool deferP = defer && !tailPass;
+        a.base = defer ? (tailPass ? nDef : p * Gd) : p * G;
+        a.G = defer ? (tailPass ? nchunks - nDef : (nDef - a.base < Gd ? nDef - a.base : Gd)) : G;
         a.inter = buf;
         a.units = (DecUnit*)(buf + G * stride);
-        a.jobs = defer ? buf + G * stride + unitBytes : nullptr;
+        a.jobs = deferP ? buf + G * stride + unitBytes : nullptr;
+        // the last deferred pass's sections: nothing after them overlaps their chains
+        a.hufPrio = (deferP && c->hufPrioLast && (p + 1 == passes || (p + 2 == passes && nDef < nchunks))) ? 1u : 0u;
         c->lastUnits = a.units;
-        c->lastG = G;
-        a.base = p * G;
+        c->lastG = a.G;
         a.queue = c->qCur + p;
         if (p >= nbuf) HIPCHK(hipStreamWaitEvent(s, c->evDFree[b], 0));
         a.coopParse = (coop && codec != kCodecVbz) ? 1u : 0u;
@@ -2421,8 +2496,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         }
         // the deferred sections (kHufFrames frames of one stream type per wave), ahead of the pass's
         // merge: they overlap the next pass's frame decode
-        if (defer)
-            hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, hs, a);
+        if (deferP)
+            hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((a.G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, hs, a);
         // with deferred sections over several passes the merge goes to the third stream behind its
         // pass's sections (so it overlaps the next pass's sections); the buffer is free after it
         hipStream_t ms = hs;
@@ -2923,11 +2998,9 @@ struct StageHdr {
 // One chunk from host memory: header and samples staged in the pinned mirror and uploaded in one
 // copy; the kernels write the blob, its size, status and stats straight into the pinned mirror
 // (no copies back: the call's tail is the kernels and one wait); the blob leaves it by memcpy.
-static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap,
-                           size_t* out_size)
+static int compress_signal_one(int codec, pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap,
+                               size_t* out_size)
 {
-    if (!c || (!samples && n) || !dst || !out_size) return PGN_ERR_INVALID_ARG;
-    if (n > PGN_MAX_CHUNK_SAMPLES) return PGN_ERR_UNSUPPORTED;
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
     const size_t hdrB = 256, inB = align_up(2 * n + 16, 256);
@@ -2954,10 +3027,8 @@ static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t
     return PGN_OK;
 }
 
-static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
+static int decompress_signal_one(int codec, pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
 {
-    if (!c || (!src && len) || (!dst && n)) return PGN_ERR_INVALID_ARG;
-    if (n > PGN_MAX_CHUNK_SAMPLES) return PGN_ERR_UNSUPPORTED;
     const size_t hdrB = 256, inB = align_up(len + 16, 256);
     std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(hipSetDevice(c->device));
@@ -2981,6 +3052,210 @@ static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t l
     if (hh->status != PGN_OK) return hh->status;
     if (n) memcpy(dst, c->hstage + hdrB + inB, 2 * n);
     return PGN_OK;
+}
+
+// An arena's per-request arrays (kPcHdr bytes at its start; index = the request's place in the
+// batch order): the kernels read the device mirror's copy and write the results into pinned memory.
+struct PcHdr {
+    uint64_t off0[kPcMaxReqs];     // sample offset (elements): encode from the inputs, decode from the outputs
+    uint32_t cnt[kPcMaxReqs];
+    uint64_t outOff[kPcMaxReqs];   // encode: blob offset in the outputs
+    uint64_t outCap[kPcMaxReqs];
+    uint64_t inOff[kPcMaxReqs];    // decode: blob offset in the inputs
+    uint64_t inSize[kPcMaxReqs];
+    uint64_t outSize[kPcMaxReqs];  // results
+    int32_t status[kPcMaxReqs];
+    uint64_t stats[kPcMaxReqs * PGN_STATS_PER_CHUNK];
+};
+static_assert(sizeof(PcHdr) <= kPcHdr, "per-request arrays");
+
+static int pc_init(pgn_ctx* c)
+{
+    HIPCHK(hipSetDevice(c->device));
+    for (PcArena& A : c->pcA) {
+        HIPCHK(hipHostMalloc((void**)&A.h, kPcHdr + kPcInCap + kPcOutCap, hipHostMallocDefault));
+        HIPCHK(hipHostGetDevicePointer((void**)&A.hDev, A.h, 0));
+        HIPCHK(hipMalloc(&A.d, kPcHdr + kPcInCap));
+    }
+    return PGN_OK;
+}
+
+// One arena's requests as one batch per (direction, codec) group, each group a batched launch over
+// the arena's arrays; one upload, one wait.  Called by the leader without pcMu.
+static void pc_run(pgn_ctx* c, PcArena& A)
+{
+    const int k = A.nreq;
+    PcReq* ord[kPcMaxReqs];
+    for (int i = 0; i < k; i++) ord[i] = A.reqs[i];
+    std::stable_sort(ord, ord + k, [](const PcReq* x, const PcReq* y) {
+        return x->dir * 16 + x->codec < y->dir * 16 + y->codec;
+    });
+    PcHdr* hh = (PcHdr*)A.h;
+    for (int i = 0; i < k; i++) {
+        const PcReq& r = *ord[i];
+        hh->cnt[i] = r.n;
+        hh->status[i] = -1;
+        hh->outSize[i] = 0;
+        if (r.dir == 0) {
+            hh->off0[i] = r.inOff / 2;
+            hh->outOff[i] = r.outOff;
+            hh->outCap[i] = r.cap;
+        } else {
+            hh->off0[i] = r.outOff / 2;
+            hh->inOff[i] = r.inOff;
+            hh->inSize[i] = r.inBytes;
+        }
+    }
+    const PcHdr* dh = (const PcHdr*)A.d;  // the device mirror of the arrays
+    PcHdr* ho = (PcHdr*)A.hDev;           // results straight into pinned memory
+    uint8_t* const inD = A.d + kPcHdr;
+    uint8_t* const outH = A.hDev + kPcHdr + kPcInCap;
+    int rc = PGN_OK;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        if (hipSetDevice(c->device) != hipSuccess ||
+            hipMemcpyAsync(A.d, A.h, kPcHdr + A.inUsed, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            rc = PGN_ERR_HIP;
+        for (int i0 = 0; rc == PGN_OK && i0 < k;) {
+            int i1 = i0;
+            uint32_t maxN = 1;
+            while (i1 < k && ord[i1]->dir == ord[i0]->dir && ord[i1]->codec == ord[i0]->codec) {
+                maxN = ord[i1]->n > maxN ? ord[i1]->n : maxN;
+                i1++;
+            }
+            const size_t m = (size_t)(i1 - i0);
+            if (ord[i0]->dir == 0)
+                rc = launch_encode(c, ord[i0]->codec, m, (const int16_t*)inD, dh->off0 + i0, dh->cnt + i0, outH,
+                                   dh->outOff + i0, dh->outCap + i0, ho->outSize + i0, ho->status + i0,
+                                   ho->stats + (size_t)i0 * PGN_STATS_PER_CHUNK, c->stream, maxN);
+            else
+                rc = launch_decode(c, ord[i0]->codec, m, inD, dh->inOff + i0, dh->inSize + i0, (int16_t*)outH,
+                                   dh->off0 + i0, dh->cnt + i0, ho->status + i0, c->stream, maxN);
+            i0 = i1;
+        }
+        if (hipStreamSynchronize(c->stream) != hipSuccess && rc == PGN_OK) rc = PGN_ERR_HIP;
+    }
+    for (int i = 0; i < k; i++) {
+        PcReq& r = *ord[i];
+        r.rc = rc != PGN_OK ? rc : hh->status[i];
+        r.outSize = hh->outSize[i];
+    }
+}
+
+enum { kPcExclusive = 1000 };  // the call runs on its own (too large for an arena, or no arenas)
+
+// A per-chunk host call through the arenas (see PcArena).  Returns the call's status, or
+// kPcExclusive when it should run by itself.
+static int pc_call(pgn_ctx* c, PcReq& r)
+{
+    const size_t inB = align_up(r.inBytes + 16, 256), outB = align_up(r.outBytes + 64, 256);
+    if (inB > kPcInCap || outB > kPcOutCap) return kPcExclusive;
+    std::unique_lock<std::mutex> lk(c->pcMu);
+    if (c->pcReady == 0) c->pcReady = pc_init(c) == PGN_OK ? 1 : -1;
+    if (c->pcReady < 0) return kPcExclusive;
+    PcArena* A = nullptr;
+    while (true) {  // join the open arena when it has room
+        if (c->pcOpen >= 0) {
+            PcArena& O = c->pcA[c->pcOpen];
+            if (O.nreq < kPcMaxReqs && O.inUsed + inB <= kPcInCap && O.outUsed + outB <= kPcOutCap) {
+                A = &O;
+                break;
+            }
+        }
+        c->pcCv.wait(lk);
+    }
+    const int ai = (int)(A - c->pcA);
+    r.inOff = A->inUsed;
+    r.outOff = A->outUsed;
+    A->inUsed += inB;
+    A->outUsed += outB;
+    A->reqs[A->nreq++] = &r;
+    A->unstaged++;
+    r.done = false;
+    lk.unlock();
+    if (r.inBytes) memcpy(A->h + kPcHdr + r.inOff, r.in, r.inBytes);
+    lk.lock();
+    if (--A->unstaged == 0) c->pcCv.notify_all();
+    while (!r.done) {
+        if (!c->pcBusy && A->state == 0) {  // lead: run this arena (it holds this call)
+            c->pcBusy = true;
+            A->state = 1;
+            PcArena& B = c->pcA[1 - ai];
+            c->pcOpen = (B.state == 0 && B.nreq == 0) ? 1 - ai : -1;  // new calls fill the other arena
+            c->pcCv.notify_all();
+            while (A->unstaged) c->pcCv.wait(lk);
+            lk.unlock();
+            pc_run(c, *A);
+            lk.lock();
+            A->state = 2;
+            A->readers = A->nreq;
+            for (int i = 0; i < A->nreq; i++) A->reqs[i]->done = true;
+            c->pcBusy = false;
+            c->pcCv.notify_all();
+        } else {
+            c->pcCv.wait(lk);
+        }
+    }
+    lk.unlock();
+    const uint8_t* res = A->h + kPcHdr + kPcInCap + r.outOff;
+    if (r.rc == PGN_OK) {
+        if (r.dir == 0) memcpy(r.dst, res, (size_t)r.outSize);
+        else if (r.n) memcpy(r.dst, res, 2 * (size_t)r.n);
+    }
+    lk.lock();
+    if (--A->readers == 0) {  // the arena is idle again
+        A->state = 0;
+        A->nreq = 0;
+        A->inUsed = A->outUsed = 0;
+        if (c->pcOpen < 0) c->pcOpen = ai;
+        c->pcCv.notify_all();
+    }
+    return r.rc;
+}
+
+// The blob bytes an encode call can need: its five frames (each at most ZSTD_COMPRESSBOUND of its
+// stream, the streams together at most 3.75 n bytes; VBZ: one frame of ~2.13 n) and their prefixes.
+static size_t pc_enc_out_bytes(size_t n, size_t cap)
+{
+    const size_t b = 4 * n + 4096;
+    return cap < b ? cap : b;
+}
+
+static int compress_signal(int codec, pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap,
+                           size_t* out_size)
+{
+    if (!c || (!samples && n) || !dst || !out_size) return PGN_ERR_INVALID_ARG;
+    if (n > PGN_MAX_CHUNK_SAMPLES) return PGN_ERR_UNSUPPORTED;
+    PcReq r{};
+    r.dir = 0;
+    r.codec = codec;
+    r.in = samples;
+    r.inBytes = 2 * n;
+    r.n = (uint32_t)n;
+    r.dst = dst;
+    r.cap = cap;
+    r.outBytes = pc_enc_out_bytes(n, cap);
+    const int rc = pc_call(c, r);
+    if (rc == kPcExclusive) return compress_signal_one(codec, c, samples, n, dst, cap, out_size);
+    *out_size = (size_t)r.outSize;
+    return rc;
+}
+
+static int decompress_signal(int codec, pgn_ctx* c, const uint8_t* src, size_t len, int16_t* dst, size_t n)
+{
+    if (!c || (!src && len) || (!dst && n)) return PGN_ERR_INVALID_ARG;
+    if (n > PGN_MAX_CHUNK_SAMPLES) return PGN_ERR_UNSUPPORTED;
+    PcReq r{};
+    r.dir = 1;
+    r.codec = codec;
+    r.in = src;
+    r.inBytes = len;
+    r.n = (uint32_t)n;
+    r.dst = dst;
+    r.outBytes = 2 * n;
+    const int rc = pc_call(c, r);
+    if (rc == kPcExclusive) return decompress_signal_one(codec, c, src, len, dst, n);
+    return rc;
 }
 
 int pgn_compress_signal(pgn_ctx* c, const int16_t* samples, size_t n, uint8_t* dst, size_t cap, size_t* out_size)

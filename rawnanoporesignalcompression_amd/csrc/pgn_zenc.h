@@ -590,13 +590,32 @@ __device__ __noinline__ SearchOut fast_search_wave(const uint8_t* __restrict__ s
         chain = 0;
         ci = 0;
         if (ip0 <= ilimit) {
+            // what this tail and the next round read, in flight together: the two new table entries'
+            // words, the repeat-offset check's words and the next round's visits (valid unless a
+            // repeat match moves the anchor and swaps the offsets) -- one memory round trip, not three
+            uint64_t wa = 0, wb = 0;
             if (lane == 0) {
-                const uint64_t wa = ld64u(src + cur0 + 1), wb = ld64u(src + ip0 - 2);
+                wa = ld64u(src + cur0 + 1);
+                wb = ld64u(src + ip0 - 2);
+            }
+            uint32_t rc0 = 0, rc1 = 0;
+            if (off2 > 0) {
+                rc0 = ld32u(src + ip0);
+                rc1 = ld32u(src + ip0 - (int32_t)off2);
+            }
+            positions(0, pk, pNext);
+            loads(pk, v8, repw);
+            havePk = true;
+            if (lane == 0) {
                 gst<uint32_t>(ht + z1::hash_word(wa, hlog, mls), ht_entry(tag, cur0 + 2, (uint32_t)wa, idxBits));
                 gst<uint32_t>(ht + z1::hash_word(wb, hlog, mls), ht_entry(tag, (uint32_t)(ip0 - 2) + 1, (uint32_t)wb, idxBits));
             }
             if (off2 > 0) {
-                while ((ip0 <= ilimit) && (ld32u(src + ip0) == ld32u(src + ip0 - (int32_t)off2))) {
+                bool firstRep = true;
+                while ((ip0 <= ilimit) &&
+                       (firstRep ? rc0 == rc1 : ld32u(src + ip0) == ld32u(src + ip0 - (int32_t)off2))) {
+                    firstRep = false;
+                    havePk = false;  // the anchor moves and the offsets swap
                     const uint32_t rLength = wave_match_count(src, (uint32_t)ip0 + 4, (uint32_t)ip0 + 4 - off2, (uint32_t)iend) + 4;
                     const uint32_t t = off2;
                     off2 = off1;

@@ -19,18 +19,21 @@ import _oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def dcodec():
+@pytest.fixture(scope="module", params=[0, 40], ids=["all_deferred", "plain_tail"])
+def dcodec(request):
+    """Passes of 96 chunks; with plain_tail the last 40 chunks of a call are one pass whose Huffman
+    sections dec_zstd_kernel decodes in place (PGN_DEFER_TAIL_PLAIN)."""
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from rawnanoporesignalcompression_amd import PGNanoCodec
 
-    keys = ("PGN_DEFER_MIN_CHUNKS", "PGN_DEFER_G")
+    keys = ("PGN_DEFER_MIN_CHUNKS", "PGN_DEFER_G", "PGN_DEFER_TAIL_PLAIN")
     old = {k: os.environ.get(k) for k in keys}
     os.environ["PGN_DEFER_MIN_CHUNKS"] = "1"
     os.environ["PGN_DEFER_G"] = "96"
+    os.environ["PGN_DEFER_TAIL_PLAIN"] = str(request.param)
     try:
         c = PGNanoCodec(0)
     finally:
