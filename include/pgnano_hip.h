@@ -31,11 +31,10 @@ typedef enum pgn_status {
     PGN_ERR_ZSTD_COMPRESS = 5,    /* "Failed to compress ..."                        C5.hpp:340-342 */
     PGN_ERR_CORRUPT = 6,          /* input on which the reference reads out of bounds (UB there) */
     PGN_ERR_ALLOC = 8,            /* decode: the frames' content sizes sum to more than 2^40 bytes, taken as the
-                                     reference's allocation of that intermediate failing (C5.hpp:575-583) */
-    PGN_ERR_UNSUPPORTED = 9,      /* chunk above PGN_MAX_CHUNK_SAMPLES; decode: frames claiming more content than
-                                     2.25 bytes per sample + 1,024 of the call's largest chunk (the intermediate's
-                                     capacity) that their blocks could really produce (a claim the blocks cannot
-                                     reach is "failed to decompress", as ZSTD_decompress reports it) */
+                                     reference's allocation of that intermediate failing (C5.hpp:575-583); also
+                                     a chunk whose frames could really expand to more than 1 GiB (the claims pass's
+                                     intermediate limit, see the decode notes below) */
+    PGN_ERR_UNSUPPORTED = 9,      /* chunk above PGN_MAX_CHUNK_SAMPLES */
     PGN_ERR_INVALID_ARG = 10,
     PGN_ERR_HIP = 11,             /* HIP runtime failure (message in pgn_last_error) */
     PGN_ERR_NO_DEVICE = 12,
@@ -52,7 +51,11 @@ typedef enum pgn_status {
  * call whose per-chunk buffers are spaced for the largest of them (see the batch calls below).
  * Decode: a chunk's decoded frames share an intermediate buffer of 2.25 bytes per sample + 1,024 of
  * the call's largest chunk (262,144 samples when the call gives no bound): every blob whose frames
- * decode to what its merge consumes fits it.  Frames claiming more: see PGN_ERR_UNSUPPORTED. */
+ * decode to what its merge consumes fits it.  Frames whose content sizes claim more are decoded as the
+ * reference decodes them -- each into exactly its claim, in an intermediate of the claims' sum -- by a
+ * second pass of the same call (a claim the frame's blocks cannot produce is "failed to decompress",
+ * as ZSTD_decompress reports it, without decoding); so a chunk's status does not depend on the other
+ * chunks of its call. */
 #define PGN_MAX_CHUNK_SAMPLES 16777216u
 
 /* Per-chunk statistics, the reference's global byte counters (src/c++/copy.cpp:64-85, updated at
@@ -108,9 +111,11 @@ int pgn_pod5_vbz_decompress_signal(const char *compressed_signal, size_t compres
  * capacity d_out_caps[i]; d_out_sizes[i] and d_status[i] receive the result.  d_stats (optional)
  * receives PGN_STATS_PER_CHUNK uint64 per chunk.
  * The batch calls are asynchronous on `stream` except for one host wait: the chunks above 262,144
- * samples are listed by a small kernel that runs after the work queued before the call (while the
- * batched pass runs) and the host reads their count before queueing their pass.  The wait ends when
- * the earlier work and that kernel have finished, not the call's own kernels. */
+ * samples (and, when decoding, the chunks whose frames claim more than the batched pass's
+ * intermediates) are listed by a small kernel that runs after the work queued before the call (while
+ * the batched pass runs) and the host reads their count before queueing their pass.  The wait ends
+ * when the earlier work and that kernel have finished, not the call's own kernels.  The _bounded
+ * variants below skip it. */
 int pgn_compress_batch_device(pgn_ctx *ctx, size_t nchunks, const int16_t *d_samples,
                               const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts, uint8_t *d_out,
                               const uint64_t *d_out_offsets, const uint64_t *d_out_caps, uint64_t *d_out_sizes,
@@ -121,6 +126,23 @@ int pgn_compress_batch_device(pgn_ctx *ctx, size_t nchunks, const int16_t *d_sam
 int pgn_decompress_batch_device(pgn_ctx *ctx, size_t nchunks, const uint8_t *d_in, const uint64_t *d_in_offsets,
                                 const uint64_t *d_in_sizes, int16_t *d_samples, const uint64_t *d_sample_offsets,
                                 const uint32_t *d_sample_counts, int32_t *d_status, void *stream);
+
+/* The batch calls with the caller's bound on the chunk sizes (max_chunk_samples >= every
+ * d_sample_counts[i], e.g. the writer's chunk size, file_writer.h:22): with a bound at or below
+ * 262,144 samples no scan runs and the call never waits on the host; the decode intermediates are
+ * spaced for the bound.  A chunk above the bound may get PGN_ERR_UNSUPPORTED.  Decode: a chunk whose
+ * frames claim more than 2.25 x the bound + 1,024 bytes and could really produce it gets
+ * PGN_ERR_UNSUPPORTED here (listing it needs the host wait; the unbounded call decodes it as the
+ * reference does). */
+int pgn_compress_batch_device_bounded(pgn_ctx *ctx, uint32_t max_chunk_samples, size_t nchunks,
+                                      const int16_t *d_samples, const uint64_t *d_sample_offsets,
+                                      const uint32_t *d_sample_counts, uint8_t *d_out, const uint64_t *d_out_offsets,
+                                      const uint64_t *d_out_caps, uint64_t *d_out_sizes, int32_t *d_status,
+                                      uint64_t *d_stats, void *stream);
+int pgn_decompress_batch_device_bounded(pgn_ctx *ctx, uint32_t max_chunk_samples, size_t nchunks, const uint8_t *d_in,
+                                        const uint64_t *d_in_offsets, const uint64_t *d_in_sizes, int16_t *d_samples,
+                                        const uint64_t *d_sample_offsets, const uint32_t *d_sample_counts,
+                                        int32_t *d_status, void *stream);
 
 /* ---- VBZ: the pod5 baseline codec (svb16 + zstd level 1), same context, same conventions ------
  * pod5::compressed_signal_max_size (signal_compression.cpp:14-19):

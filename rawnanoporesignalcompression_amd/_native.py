@@ -50,6 +50,10 @@ SIGNATURES = [
     ("pgn_compress_batch_device", C.c_int,
      [_VP, _SZ, _VP, _U64P, _U32P, _VP, _U64P, _U64P, _U64P, _I32P, _U64P, _VP]),
     ("pgn_decompress_batch_device", C.c_int, [_VP, _SZ, _VP, _U64P, _U64P, _VP, _U64P, _U32P, _I32P, _VP]),
+    ("pgn_compress_batch_device_bounded", C.c_int,
+     [_VP, C.c_uint32, _SZ, _VP, _U64P, _U32P, _VP, _U64P, _U64P, _U64P, _I32P, _U64P, _VP]),
+    ("pgn_decompress_batch_device_bounded", C.c_int,
+     [_VP, C.c_uint32, _SZ, _VP, _U64P, _U64P, _VP, _U64P, _U32P, _I32P, _VP]),
     ("pgn_vbz_compressed_signal_max_size", C.c_size_t, [C.c_size_t]),
     ("pgn_vbz_compress_signal", C.c_int, [_VP, _VP, _SZ, _VP, _SZ, C.POINTER(C.c_size_t)]),
     ("pgn_vbz_decompress_signal", C.c_int, [_VP, _VP, _SZ, _VP, _SZ]),

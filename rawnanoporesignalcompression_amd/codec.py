@@ -126,6 +126,12 @@ class PGNanoCodec:
             return getattr(self._lib, self._VARIANT_FN[fn])(self._h, _native.VARIANTS[self.variant], *args)
         return getattr(self._lib, fn)(self._h, *args)
 
+    def _bounded(self, fn: str, bound: int, *args):
+        """The C5 batch calls with a chunk-size bound (pgnano_hip.h *_bounded)."""
+        if type(self) is not PGNanoCodec or getattr(self, "variant", "C5") != "C5":
+            raise ValueError("max_chunk_samples: the bounded batch calls are C5's")
+        return getattr(self._lib, fn)(self._h, bound, *args)
+
     def _launch_stream(self, stream):
         """The HIP stream a batch call runs on (the caller's, else the context's), made to wait for
         the caller's current stream.  The call's own allocations and fills are issued on it too, so
@@ -168,11 +174,14 @@ class PGNanoCodec:
 
     # ---- batched device API -----------------------------------------------------------------
     def compress_batch(self, samples, sample_offsets, sample_counts, with_stats: bool = False,
-                       out=None, out_offsets=None, out_caps=None, stream: int | None = None) -> EncodedBatch:
+                       out=None, out_offsets=None, out_caps=None, stream: int | None = None,
+                       max_chunk_samples: int | None = None) -> EncodedBatch:
         """Encode every chunk of a device-resident batch in one launch.
 
         samples: int16 cuda tensor; sample_offsets: int64 tensor (elements); sample_counts: int32.
         Blobs land at ``out_offsets`` (default: packed with compressed_signal_max_size capacities).
+        max_chunk_samples: the caller's bound on the chunk sizes (pgn_compress_batch_device_bounded:
+        no host wait when it is at most 262,144).
         """
         import torch
 
@@ -202,15 +211,19 @@ class PGNanoCodec:
             sizes = torch.zeros(n, dtype=torch.int64, device=dev)
             status = torch.full((n,), -1, dtype=torch.int32, device=dev)
             stats = torch.zeros((n, _native.PGN_STATS_PER_CHUNK), dtype=torch.int64, device=dev) if with_stats else None
-            _check(self._call(
-                self._fn_compress_batch, n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
-                _ptr(status), _ptr(stats), ls.cuda_stream))
+            args = (n, _ptr(samples), _ptr(offs), _ptr(counts), _ptr(out), _ptr(oo), _ptr(caps), _ptr(sizes),
+                    _ptr(status), _ptr(stats), ls.cuda_stream)
+            if max_chunk_samples is not None:
+                _check(self._bounded("pgn_compress_batch_device_bounded", int(max_chunk_samples), *args))
+            else:
+                _check(self._call(self._fn_compress_batch, *args))
         caller.wait_stream(ls)
         return EncodedBatch(out, oo, caps, sizes, status, stats)
 
     def decompress_batch(self, blobs, blob_offsets, blob_sizes, sample_counts, out=None, out_offsets=None,
-                         stream: int | None = None):
-        """Decode a device-resident batch; returns (samples int16 tensor, offsets, status)."""
+                         stream: int | None = None, max_chunk_samples: int | None = None):
+        """Decode a device-resident batch; returns (samples int16 tensor, offsets, status).
+        max_chunk_samples: as in :meth:`compress_batch` (pgn_decompress_batch_device_bounded)."""
         import torch
 
         _require_device(blobs, "blobs", self.device)
@@ -234,9 +247,11 @@ class PGNanoCodec:
             bo = blob_offsets.to(device=dev, dtype=torch.int64).contiguous()
             bs = blob_sizes.to(device=dev, dtype=torch.int64).contiguous()
             status = torch.full((n,), -1, dtype=torch.int32, device=dev)
-            _check(self._call(
-                self._fn_decompress_batch, n, _ptr(blobs), _ptr(bo), _ptr(bs), _ptr(out), _ptr(so), _ptr(counts),
-                _ptr(status), ls.cuda_stream))
+            args = (n, _ptr(blobs), _ptr(bo), _ptr(bs), _ptr(out), _ptr(so), _ptr(counts), _ptr(status), ls.cuda_stream)
+            if max_chunk_samples is not None:
+                _check(self._bounded("pgn_decompress_batch_device_bounded", int(max_chunk_samples), *args))
+            else:
+                _check(self._call(self._fn_decompress_batch, *args))
         caller.wait_stream(ls)
         return out, so, status
 

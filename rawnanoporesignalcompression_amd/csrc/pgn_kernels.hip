@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <condition_variable>
 #include <mutex>
+#include <vector>
 
 #include "../../include/pgnano_hip.h"
 #include "../../include/pgnano_pod5.h"
@@ -505,6 +506,7 @@ struct DecArgs {
     uint32_t coopParse;  // dec_zstd_coop_kernel parses the chunks itself (no dec_parse_kernel launch)
     uint8_t* jobs;       // [G][5] HufJob records (pgn_hufjob.h): dec_zstd_kernel defers, dec_huf_kernel decodes; null = in place
     uint32_t hufPrio;    // dec_huf_kernel waves at raised priority (the last deferred pass: the decode's drain)
+    uint64_t interBytes; // dec_chunk_kernel's claims pass: the slot intermediate's bytes (0: inter_cap(capN))
 };
 
 // The status of a chunk whose frames claim more content (ZSTD_getFrameContentSize) than the
@@ -515,14 +517,85 @@ struct DecArgs {
 // z1::frame_content_bound); only frames that could really expand that far are PGN_ERR_UNSUPPORTED.
 __device__ inline int over_claim_status(const uint8_t* in, const DecUnit* u, const uint64_t* cs, int nf)
 {
-    uint64_t tot = 0;
-    for (int s = 0; s < nf; s++) tot += cs[s];
+    uint64_t tot = 0;  // each claim capped just above the limit: five claims near 2^64 cannot wrap below it
+    for (int s = 0; s < nf; s++) tot += cs[s] <= kAllocLimit ? cs[s] : kAllocLimit + 1;
     if (tot > kAllocLimit) return PGN_ERR_ALLOC;
     for (int s = 0; s < nf; s++) {
         const int64_t b = z1::frame_content_bound(in + u[s].src, (size_t)u[s].len);
         if (b < 0 || (uint64_t)b < cs[s]) return PGN_ERR_ZSTD_DECOMPRESS;
     }
     return PGN_ERR_UNSUPPORTED;
+}
+
+// The claims pass (launch_claims_decode) decodes the chunks over_claim_status leaves UNSUPPORTED, as
+// the reference does: every frame into exactly its claim, in an intermediate of the claims' sum.  A
+// chunk whose sum exceeds kClaimPassMax gets PGN_ERR_ALLOC (that intermediate does not fit the
+// device's budget, the reference's allocation failing) -- only a blob built to expand (its blocks'
+// bound is at most 32,768 times its length) reaches it.
+constexpr uint64_t kClaimPassMax = (uint64_t)1 << 30;
+
+// A blob of nf frames behind nf - 1 eight-byte length prefixes (C5.hpp:530-586; the variants'
+// decompress_signal_* the same with fewer frames): false when it does not parse that far (the
+// decoders' PGN_ERR_CORRUPT / PGN_ERR_NOT_ZSTD); else the claims' sum and largest claim, and
+// *expand = the claims sum to at most 2^40 and every frame's blocks could produce its claim
+// (z1::frame_content_bound) -- the chunks over_claim_status calls UNSUPPORTED when they exceed a
+// decoder's buffer.
+__host__ __device__ inline bool blob_claims(const uint8_t* src, uint64_t len, int nf, uint64_t* sum, uint64_t* maxClaim,
+                                            bool* expand)
+{
+    uint64_t pos = 0, tot = 0, mx = 0, fo[kStreams], fl[kStreams], cs[kStreams];
+    for (int s = 0; s < nf; s++) {
+        uint64_t l;
+        if (s < nf - 1) {
+            if (pos > len || len - pos < 8) return false;
+            memcpy(&l, src + pos, 8);
+            pos += 8;
+            if (l > len - pos) return false;
+        } else {
+            l = len - pos;
+        }
+        bool ok = false;
+        cs[s] = z1::frame_content_size(src + pos, (size_t)l, &ok);
+        if (!ok) return false;
+        fo[s] = pos;
+        fl[s] = l;
+        tot += cs[s] <= kAllocLimit ? cs[s] : kAllocLimit + 1;  // capped: five claims cannot wrap
+        mx = cs[s] > mx ? cs[s] : mx;
+        pos += l;
+    }
+    bool ex = tot <= kAllocLimit;
+    for (int s = 0; ex && s < nf; s++) {
+        const int64_t b = z1::frame_content_bound(src + fo[s], (size_t)fl[s]);
+        ex = b >= 0 && (uint64_t)b >= cs[s];
+    }
+    *sum = tot;
+    *maxClaim = mx;
+    *expand = ex;
+    return true;
+}
+// a chunk of n samples the claims pass must decode: its frames claim more than any decoder buffer
+// spaced for n samples holds (inter_cap(n) less the VBZ padding, or one frame above n bytes: the C5
+// per-stream bound) and could really produce it
+__host__ __device__ inline bool claims_pass_chunk(const uint8_t* src, uint64_t len, int nf, uint32_t n, uint64_t* sum)
+{
+    uint64_t mx = 0;
+    bool ex = false;
+    if (!blob_claims(src, len, nf, sum, &mx, &ex) || !ex) return false;
+    return *sum + kVbzPadding > inter_cap(n) || mx > n;
+}
+
+// Unhinted batch decodes: the chunks for the claims pass, listed on the scan stream beside the
+// batched pass (hdr[4] count, hdr[5] the largest claims' sum in KiB, capped at 2^32 - 1).
+__global__ void claim_scan_kernel(const uint8_t* in, const uint64_t* inOffsets, const uint64_t* inSizes,
+                                  const uint32_t* counts, size_t n, int nf, uint32_t* list, uint32_t* hdr)
+{
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t sum = 0;
+        if (!claims_pass_chunk(in + inOffsets[i], inSizes[i], nf, counts[i], &sum)) continue;
+        list[atomicAdd(hdr + 4, 1u)] = (uint32_t)i;
+        const uint64_t kib = (sum + 1023) >> 10;
+        atomicMax(hdr + 5, kib < 0xFFFFFFFFull ? (uint32_t)kib : 0xFFFFFFFFu);
+    }
 }
 
 // one thread per chunk: the four length prefixes and the five frame headers (C5.hpp:530-586).
@@ -1600,10 +1673,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void de
         int16_t* out = a.samples + a.sampleOffsets[c];
         DecUnit d[kStreams];
         uint64_t total = 0;
-        int st = n > capN ? PGN_ERR_UNSUPPORTED  // the large-chunk pass takes it
-                          : __builtin_amdgcn_readfirstlane(
-                                parse_frames<nf>(a.in, a.inOffsets[c], a.inSizes[c], d, &total, inter_cap(capN)));
-        if (Codec == kCodecC5 && st == PGN_OK) {  // C5: the staged path's per-stream bound
+        // the claims pass (a.interBytes): any sample count, the frames in an intermediate sized from
+        // the listed chunks' claims; a chunk claiming more than it is the claims pass's ALLOC
+        const bool claims = a.interBytes != 0;
+        int st = (n > capN && !claims) ? PGN_ERR_UNSUPPORTED  // the large-chunk pass takes it
+                                       : __builtin_amdgcn_readfirstlane(parse_frames<nf>(
+                                             a.in, a.inOffsets[c], a.inSizes[c], d, &total,
+                                             claims ? (size_t)a.interBytes : inter_cap(capN)));
+        if (claims && st == PGN_ERR_UNSUPPORTED) st = PGN_ERR_ALLOC;
+        if (Codec == kCodecC5 && st == PGN_OK && !claims) {  // C5: the staged path's per-stream bound
             uint64_t cs64[kStreams];
             bool over = false;
 #pragma unroll
@@ -1818,6 +1896,7 @@ struct pgn_ctx {
     // A deferred pass ends with one lane's ~16,000-symbol chain per M stream, which nothing overlaps
     // once the frame decode of the last pass is done (the decode's drain)
     size_t deferTailPlain = 0;
+    size_t deferHead = 0;      // PGN_DEFER_HEAD: chunks of a short first deferred pass (0 = balanced passes)
     bool hufPrioLast = false;  // PGN_HUF_PRIO_LAST=1: the last deferred pass's dec_huf waves at raised priority
     bool lastDeferred = false;  // the last staged C5 decode deferred its Huffman sections (pgn_ctx_kernels)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
@@ -1877,8 +1956,10 @@ struct pgn_ctx {
     // batched pass runs; slot scratch spaced for the largest chunk, and its own table epochs and
     // work counter.
     uint32_t* largeList = nullptr;
+    uint32_t* claimList = nullptr;     // the claims pass's chunks (claim_scan_kernel, or from the host)
     size_t largeListCap = 0;
-    uint32_t* largeHdr = nullptr;      // [0..1] header, [2] the large pass's work counter
+    uint32_t* largeHdr = nullptr;      // [0..1] header, [2] the large pass's work counter, [3] largest chunk,
+                                       // [4..5] the claims pass's count and largest sum (KiB)
     uint32_t* largeHdrHost = nullptr;
     hipStream_t scanStream = nullptr;
     hipEvent_t evScanFork = nullptr, evScan = nullptr;
@@ -1988,6 +2069,7 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     }
     if (const char* v = getenv("PGN_DEFER_MIN_CHUNKS")) { const long x = atol(v); if (x > 0) c->deferMin = (size_t)x; }
     if (const char* v = getenv("PGN_DEFER_G")) { const long x = atol(v); if (x > 0) c->deferG = (size_t)x; }
+    if (const char* v = getenv("PGN_DEFER_HEAD")) { const long x = atol(v); if (x >= 0) c->deferHead = (size_t)x; }
     if (const char* v = getenv("PGN_HUF_PRIO_LAST")) c->hufPrioLast = v[0] == '1';
     if (const char* v = getenv("PGN_DEFER_TAIL_PLAIN")) { const long x = atol(v); if (x >= 0) c->deferTailPlain = (size_t)x; }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -2019,8 +2101,8 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     HIPCHK(hipStreamCreateWithFlags(&c->scanStream, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&c->evScanFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->evScan, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&c->largeHdr, 4 * sizeof(uint32_t)));
-    HIPCHK(hipHostMalloc((void**)&c->largeHdrHost, 4 * sizeof(uint32_t), hipHostMallocDefault));
+    HIPCHK(hipMalloc(&c->largeHdr, 8 * sizeof(uint32_t)));
+    HIPCHK(hipHostMalloc((void**)&c->largeHdrHost, 8 * sizeof(uint32_t), hipHostMallocDefault));
     HIPCHK(hipEventCreateWithFlags(&c->evFork, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->evJoin, hipEventDisableTiming));
     for (int i = 0; i < 2; i++) {
@@ -2060,6 +2142,7 @@ int pgn_ctx_destroy(pgn_ctx* c)
     }
     if (c->scanStream) (void)hipStreamSynchronize(c->scanStream);
     (void)hipFree(c->largeList);
+    (void)hipFree(c->claimList);
     (void)hipFree(c->largeHdr);
     (void)hipFree(c->largeScratch);
     (void)hipFree(c->largeEpochs);
@@ -2390,23 +2473,48 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     bool defer = codec == kCodecC5 && nchunks >= c->deferMin;
     const size_t stride = chunk_inter_bytes(capCall);
     size_t G = nchunks < c->subBatch ? nchunks : c->subBatch;  // chunks per pass (the buffers' capacity)
-    size_t Gd = G, nDef = nchunks;  // deferred calls: Gd chunks per deferred pass over the first nDef chunks
+    // the passes: chunks [pBase[p], pBase[p] + pCnt[p]); pPlain[p]: a deferred call's in-place tail
+    std::vector<size_t> pBase, pCnt;
+    std::vector<char> pPlain;
     if (defer) {  // up to deferG chunks per pass, and decBufs passes' buffers within kDecBufferBudget
         // (the budget's bound is at least subBatch chunks; PGN_DEFER_G below that is the tests' way to
         // run several passes on small batches)
         size_t gmax = kDecBufferBudget / (c->decBufs * (stride + kStreams * (sizeof(DecUnit) + kJobBytes)));
         gmax = gmax < c->subBatch ? c->subBatch : gmax;
         gmax = gmax < c->deferG ? gmax : c->deferG;
-        // the last deferTailPlain chunks: one pass whose sections are decoded in place (no drain of
-        // lane-per-stream chains after the last frame decode)
-        const size_t tail = c->deferTailPlain;
-        if (tail > 0 && tail <= gmax && nchunks >= 2 * tail) nDef = nchunks - tail;
-        const size_t np = (nDef + gmax - 1) / gmax;
-        Gd = (nDef + np - 1) / np;
-        const size_t tailN = nchunks - nDef;
-        G = Gd > tailN ? Gd : tailN;
+        // an optional short first pass (PGN_DEFER_HEAD: the sections start sooner), the passes of up to
+        // gmax chunks balanced over the rest, and an optional in-place tail pass (PGN_DEFER_TAIL_PLAIN)
+        size_t head = c->deferHead, tail = c->deferTailPlain;
+        if (!(head > 0 && head <= gmax && nchunks >= 4 * head)) head = 0;
+        if (!(tail > 0 && tail <= gmax && nchunks - head >= 2 * tail)) tail = 0;
+        if (head) {
+            pBase.push_back(0);
+            pCnt.push_back(head);
+            pPlain.push_back(0);
+        }
+        const size_t mid = nchunks - head - tail;
+        const size_t np = (mid + gmax - 1) / gmax;
+        const size_t Gd = (mid + np - 1) / np;
+        for (size_t b = head; b < head + mid; b += Gd) {
+            pBase.push_back(b);
+            pCnt.push_back(head + mid - b < Gd ? head + mid - b : Gd);
+            pPlain.push_back(0);
+        }
+        if (tail) {
+            pBase.push_back(nchunks - tail);
+            pCnt.push_back(tail);
+            pPlain.push_back(1);
+        }
+        G = 0;
+        for (size_t k : pCnt) G = k > G ? k : G;
+    } else {
+        for (size_t b = 0; b < nchunks; b += G) {
+            pBase.push_back(b);
+            pCnt.push_back(G);  // the kernels stop at nchunks
+            pPlain.push_back(1);
+        }
     }
-    const size_t passes = defer ? (nDef + Gd - 1) / Gd + (nDef < nchunks ? 1 : 0) : (nchunks + G - 1) / G;
+    const size_t passes = pBase.size();
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
     const size_t slots = nu * G < c->decSlotsMax ? nu * G : c->decSlotsMax;
     // few chunks: a workgroup per frame (not for the passes of a larger deferred call)
@@ -2468,16 +2576,14 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
     for (size_t p = 0; p < passes; p++) {
         const int b = (int)(p % nbuf);
         uint8_t* buf = c->decChunks + (size_t)b * bufBytes;
-        // this pass: chunks [base, base + a.G); a deferred call's last pass may be its in-place tail
-        const bool tailPass = defer && p * Gd >= nDef;
-        const bool deferP = defer && !tailPass;
-        a.base = defer ? (tailPass ? nDef : p * Gd) : p * G;
-        a.G = defer ? (tailPass ? nchunks - nDef : (nDef - a.base < Gd ? nDef - a.base : Gd)) : G;
+        const bool deferP = defer && !pPlain[p];
+        a.base = pBase[p];
+        a.G = pCnt[p];
         a.inter = buf;
         a.units = (DecUnit*)(buf + G * stride);
         a.jobs = deferP ? buf + G * stride + unitBytes : nullptr;
         // the last deferred pass's sections: nothing after them overlaps their chains
-        a.hufPrio = (deferP && c->hufPrioLast && (p + 1 == passes || (p + 2 == passes && nDef < nchunks))) ? 1u : 0u;
+        a.hufPrio = (deferP && c->hufPrioLast && (p + 1 == passes || (p + 2 == passes && pPlain[passes - 1]))) ? 1u : 0u;
         c->lastUnits = a.units;
         c->lastG = a.G;
         a.queue = c->qCur + p;
@@ -2530,26 +2636,39 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
 // largest of them.  Chunks above PGN_MAX_CHUNK_SAMPLES stay UNSUPPORTED.
 static bool need_scan(uint32_t maxHint) { return maxHint == 0 || maxHint > kPassSamples; }
 
-static int start_scan(pgn_ctx* c, size_t nchunks, const uint32_t* d_counts, hipStream_t s)
+// decode calls also list the chunks of the claims pass (claim_scan_kernel), given their blobs
+struct ScanBlobs {
+    const uint8_t* in;
+    const uint64_t* offsets;
+    const uint64_t* sizes;
+    int nf;
+};
+static int start_scan(pgn_ctx* c, size_t nchunks, const uint32_t* d_counts, hipStream_t s,
+                      const ScanBlobs* blobs = nullptr)
 {
     if (nchunks > c->largeListCap) {
         wait_last_host(c);
         (void)hipStreamSynchronize(c->scanStream);
         (void)hipFree(c->largeList);
-        c->largeList = nullptr;
+        (void)hipFree(c->claimList);
+        c->largeList = c->claimList = nullptr;
         const size_t m = nchunks < 4096 ? 4096 : nchunks;
         HIPCHK(hipMalloc(&c->largeList, 4 * m));
+        HIPCHK(hipMalloc(&c->claimList, 4 * m));
         c->largeListCap = m;
     }
     HIPCHK(hipEventRecord(c->evScanFork, s));
     HIPCHK(hipStreamWaitEvent(c->scanStream, c->evScanFork, 0));
-    HIPCHK(hipMemsetAsync(c->largeHdr, 0, 4 * sizeof(uint32_t), c->scanStream));
+    HIPCHK(hipMemsetAsync(c->largeHdr, 0, 8 * sizeof(uint32_t), c->scanStream));
     unsigned grid = (unsigned)((nchunks + 255) / 256);
     grid = grid > 1024 ? 1024 : grid;
     hipLaunchKernelGGL(large_scan_kernel, dim3(grid), dim3(256), 0, c->scanStream, d_counts, nchunks, c->largeList,
                        c->largeHdr);
+    if (blobs)
+        hipLaunchKernelGGL(claim_scan_kernel, dim3(grid), dim3(256), 0, c->scanStream, blobs->in, blobs->offsets,
+                           blobs->sizes, d_counts, nchunks, blobs->nf, c->claimList, c->largeHdr);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->largeHdrHost, c->largeHdr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->scanStream));
+    HIPCHK(hipMemcpyAsync(c->largeHdrHost, c->largeHdr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->scanStream));
     HIPCHK(hipEventRecord(c->evScan, c->scanStream));
     return PGN_OK;
 }
@@ -2679,6 +2798,79 @@ static int launch_large_decode(pgn_ctx* c, int codec, uint32_t count, uint32_t m
     return launch_dec_chunks(codec, a, slots, s);
 }
 
+// The claims pass: the listed chunks (list: device, count entries) decoded as the reference decodes
+// them -- every frame into exactly its content-size claim, in an intermediate of the claims' sum
+// (maxSum: the largest listed sum; above kClaimPassMax the chunk is PGN_ERR_ALLOC) -- then merged;
+// their statuses and samples replace the batched pass's.  The fused kernel, slot scratch of the
+// large pass (ordered after it on the stream).
+static int launch_claims_decode(pgn_ctx* c, int codec, uint32_t count, uint64_t maxSum, const uint32_t* list,
+                                const uint8_t* d_in, const uint64_t* d_in_offsets, const uint64_t* d_in_sizes,
+                                int16_t* d_samples, const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts,
+                                int32_t* d_status, hipStream_t s)
+{
+    const uint64_t cap = (maxSum < kClaimPassMax ? maxSum : kClaimPassMax) + kVbzPadding;
+    const size_t sb = dec_layout().bytes + align_up(cap + 64, 256);
+    const size_t slots = large_slots(c, count, sb, c->decFusedSlotsMax);
+    int rc = ensure_large_dec(c, sb * slots);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(c->largeHdr + 2, 0, sizeof(uint32_t), s));
+    DecArgs a{};
+    a.nchunks = count;
+    a.in = d_in;
+    a.inOffsets = d_in_offsets;
+    a.inSizes = d_in_sizes;
+    a.samples = d_samples;
+    a.sampleOffsets = d_sample_offsets;
+    a.sampleCounts = d_sample_counts;
+    a.status = d_status;
+    a.slotScratch = c->largeDecScratch;
+    a.slotBytes = sb;
+    a.prof = c->prof ? c->prof + kPhases : nullptr;
+    a.queue = c->largeHdr + 2;
+    a.capN = PGN_MAX_CHUNK_SAMPLES;
+    a.list = list;
+    a.interBytes = cap;
+    return launch_dec_chunks(codec, a, slots, s);
+}
+
+// The claims pass for chunks of a host-memory call (the blobs are in host memory too): the chunks
+// among [0, n) whose status came back PGN_ERR_UNSUPPORTED are listed on the host from their own bytes
+// (the device arrays describe the same chunks); then the pass runs and the call waits for it.
+static int claims_from_host(pgn_ctx* c, int codec, size_t n, const int32_t* status, const uint32_t* counts,
+                            const uint8_t* const* blobs, const uint64_t* blobLens, const uint8_t* d_in,
+                            const uint64_t* d_in_offsets, const uint64_t* d_in_sizes, int16_t* d_samples,
+                            const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, int32_t* d_status,
+                            hipStream_t s)
+{
+    uint32_t idx[kPcMaxReqs];
+    uint32_t k = 0;
+    uint64_t maxSum = 0;
+    const int nf = codec_frames(codec);
+    for (size_t i = 0; i < n && k < (uint32_t)kPcMaxReqs; i++) {
+        uint64_t sum = 0;
+        if (status[i] != PGN_ERR_UNSUPPORTED || counts[i] > PGN_MAX_CHUNK_SAMPLES) continue;
+        if (!claims_pass_chunk(blobs[i], blobLens[i], nf, counts[i], &sum)) continue;
+        idx[k++] = (uint32_t)i;
+        maxSum = sum > maxSum ? sum : maxSum;
+    }
+    if (k == 0) return PGN_OK;
+    if (!c->claimList || c->largeListCap < kPcMaxReqs) {
+        const size_t m = c->largeListCap > 4096 ? c->largeListCap : 4096;
+        (void)hipFree(c->claimList);
+        (void)hipFree(c->largeList);
+        c->claimList = c->largeList = nullptr;
+        HIPCHK(hipMalloc(&c->largeList, 4 * m));
+        HIPCHK(hipMalloc(&c->claimList, 4 * m));
+        c->largeListCap = m;
+    }
+    HIPCHK(hipMemcpyAsync(c->claimList, idx, 4 * k, hipMemcpyHostToDevice, s));
+    const int rc = launch_claims_decode(c, codec, k, maxSum, c->claimList, d_in, d_in_offsets, d_in_sizes, d_samples,
+                                        d_sample_offsets, d_sample_counts, d_status, s);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return PGN_OK;
+}
+
 // Every launch sequence on a context: ordered after the previous one (evLast, whatever its stream),
 // and recorded as the new last one.  ev[0..1] / ev[2..3] bracket the call's kernels.
 static int launch_encode(pgn_ctx* c, int codec, size_t nchunks, const int16_t* d_samples, const uint64_t* d_sample_offsets,
@@ -2720,7 +2912,8 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     // kPassSamples (the scan then runs beside the batched pass, and the launch stays asynchronous).
     uint32_t capCall = (!scan && maxHint) ? call_cap(maxHint) : kPassSamples;
     uint32_t count = 0, maxN = 0;
-    int rc = scan ? start_scan(c, nchunks, d_sample_counts, s) : PGN_OK;
+    const ScanBlobs blobs{d_in, d_in_offsets, d_in_sizes, codec_frames(codec)};
+    int rc = scan ? start_scan(c, nchunks, d_sample_counts, s, &blobs) : PGN_OK;
     // small calls (the per-chunk ones) keep the full capacity: a frame is then decoded up to its own
     // content size, as the reference does, and the chunk ends with its statuses (e.g. "Remaining
     // data" for samples fewer than the frames hold) rather than PGN_ERR_UNSUPPORTED
@@ -2732,6 +2925,10 @@ static int launch_decode(pgn_ctx* c, int codec, size_t nchunks, const uint8_t* d
     if (rc == PGN_OK && count)
         rc = launch_large_decode(c, codec, count, maxN, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
                                  d_sample_counts, d_status, s);
+    // the chunks whose frames claim more than the passes' intermediates hold (listed by the scan)
+    if (rc == PGN_OK && scan && c->largeHdrHost[4])
+        rc = launch_claims_decode(c, codec, c->largeHdrHost[4], (uint64_t)c->largeHdrHost[5] << 10, c->claimList, d_in,
+                                  d_in_offsets, d_in_sizes, d_samples, d_sample_offsets, d_sample_counts, d_status, s);
     if (rc == PGN_OK) {
         HIPCHK(hipEventRecord(c->ev[3], s));
         c->decTimed = true;
@@ -2774,6 +2971,24 @@ int pgn_compress_batch_device(pgn_ctx* c, size_t nchunks, const int16_t* d_sampl
 {
     return compress_batch(kCodecC5, c, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
                           d_out_caps, d_out_sizes, d_status, d_stats, stream);
+}
+
+int pgn_compress_batch_device_bounded(pgn_ctx* c, uint32_t max_chunk_samples, size_t nchunks, const int16_t* d_samples,
+                                      const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts, uint8_t* d_out,
+                                      const uint64_t* d_out_offsets, const uint64_t* d_out_caps, uint64_t* d_out_sizes,
+                                      int32_t* d_status, uint64_t* d_stats, void* stream)
+{
+    return compress_batch(kCodecC5, c, nchunks, d_samples, d_sample_offsets, d_sample_counts, d_out, d_out_offsets,
+                          d_out_caps, d_out_sizes, d_status, d_stats, stream, max_chunk_samples ? max_chunk_samples : 1u);
+}
+
+int pgn_decompress_batch_device_bounded(pgn_ctx* c, uint32_t max_chunk_samples, size_t nchunks, const uint8_t* d_in,
+                                        const uint64_t* d_in_offsets, const uint64_t* d_in_sizes, int16_t* d_samples,
+                                        const uint64_t* d_sample_offsets, const uint32_t* d_sample_counts,
+                                        int32_t* d_status, void* stream)
+{
+    return decompress_batch(kCodecC5, c, nchunks, d_in, d_in_offsets, d_in_sizes, d_samples, d_sample_offsets,
+                            d_sample_counts, d_status, stream, max_chunk_samples ? max_chunk_samples : 1u);
 }
 
 int pgn_decompress_batch_device(pgn_ctx* c, size_t nchunks, const uint8_t* d_in, const uint64_t* d_in_offsets,
@@ -3049,6 +3264,13 @@ static int decompress_signal_one(int codec, pgn_ctx* c, const uint8_t* src, size
                        n ? (uint32_t)n : 1u);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (hh->status == PGN_ERR_UNSUPPORTED) {  // frames claiming more than the intermediate: the claims pass
+        const uint8_t* bl = c->hstage + hdrB;
+        const uint64_t ln = len;
+        rc = claims_from_host(c, codec, 1, &hh->status, &hh->count, &bl, &ln, din, &d->inOff, &d->inSize, hout, &d->off0,
+                              &d->count, &hd->status, c->stream);
+        if (rc) return rc;
+    }
     if (hh->status != PGN_OK) return hh->status;
     if (n) memcpy(dst, c->hstage + hdrB + inB, 2 * n);
     return PGN_OK;
@@ -3134,6 +3356,23 @@ static void pc_run(pgn_ctx* c, PcArena& A)
             i0 = i1;
         }
         if (hipStreamSynchronize(c->stream) != hipSuccess && rc == PGN_OK) rc = PGN_ERR_HIP;
+        // decode chunks whose frames claim more than the batch's intermediates: the claims pass
+        for (int i0 = 0; rc == PGN_OK && i0 < k;) {
+            int i1 = i0;
+            while (i1 < k && ord[i1]->dir == ord[i0]->dir && ord[i1]->codec == ord[i0]->codec) i1++;
+            if (ord[i0]->dir == 1) {
+                const uint8_t* bl[kPcMaxReqs];
+                uint64_t ln[kPcMaxReqs];
+                for (int i = i0; i < i1; i++) {
+                    bl[i - i0] = A.h + kPcHdr + ord[i]->inOff;
+                    ln[i - i0] = ord[i]->inBytes;
+                }
+                rc = claims_from_host(c, ord[i0]->codec, (size_t)(i1 - i0), hh->status + i0, hh->cnt + i0, bl, ln, inD,
+                                      dh->inOff + i0, dh->inSize + i0, (int16_t*)outH, dh->off0 + i0, dh->cnt + i0,
+                                      ho->status + i0, c->stream);
+            }
+            i0 = i1;
+        }
     }
     for (int i = 0; i < k; i++) {
         PcReq& r = *ord[i];
