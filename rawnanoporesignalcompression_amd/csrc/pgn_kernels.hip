@@ -1046,6 +1046,54 @@ __global__ __launch_bounds__(64) void dec_huf_kernel(DecArgs a)
     Pp.flush();
 }
 
+// The same jobs, latency first (the last deferred pass of a call: nothing overlaps its sections
+// once the frame decode has ended -- the decode's drain).  A workgroup of four waves per job, one wave
+// per stream with all 64 lanes (huf_decode1of4_wave64, the cooperative decoder: speculative windows,
+// a sync, an exact second pass), so a stream's ~16,000 symbols take a few 64-lane rounds instead of
+// one lane's serial chain; about 2.5 times the instructions of dec_huf_kernel, on a chip that is
+// otherwise waiting.  The compact table is expanded back into the full 2^tl-entry table in LDS.  Same
+// symbols and the same strict end rule; a failing stream marks its frame kDecErrHufStream.
+__global__ __launch_bounds__(64 * kCoopWaves) void dec_huf_wide_kernel(DecArgs a)
+{
+    const uint32_t u = blockIdx.x;
+    const size_t G = a.G;
+    if ((size_t)u >= (size_t)a.nu * G) return;
+    const int s = unit_stream((uint32_t)(u / G));  // large streams first
+    const size_t g = u % G;
+    if (a.base + g >= a.nchunks) return;
+    const HufJob* J = (const HufJob*)(a.jobs + (g * kStreams + (size_t)s) * kJobBytes);
+    if (gld<uint32_t>(&J->flag) == 0) return;  // the same for every wave of the group
+    __shared__ uint32_t stgAll[kCoopWaves * kCoopStgWords];
+    __shared__ uint32_t bad;
+    const uint32_t tid = threadIdx.x;
+    const int wid = (int)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t hp = gld<uint64_t>(&J->hp), dstp = gld<uint64_t>(&J->dst);
+    const uint4 len = gld<uint4>(&J->len[0]);
+    const uint4 prm = gld<uint4>(&J->rs);
+    const uint32_t C2 = gld<uint32_t>(&J->C2);
+    const uint32_t rs = prm.x, tl = prm.y, d1 = prm.z & 0xFFu, d2 = prm.z >> 8, C1 = prm.w;
+    // the full table from the compact one: entry min(p, (p >> d1) + C1, (p >> d2) + C2), swapped back
+    // to symbol | nbBits << 8
+    const uint16_t* ct = (const uint16_t*)(a.jobs + (g * kStreams + (size_t)s) * kJobBytes + sizeof(HufJob));
+    for (uint32_t p = tid; p < (1u << tl); p += 64 * kCoopWaves) {
+        const uint32_t i1 = (p >> d1) + C1, i2 = (p >> d2) + C2;
+        uint32_t i = p < i1 ? p : i1;
+        i = i < i2 ? i : i2;
+        const uint32_t c = gld<uint16_t>(ct + i);
+        sDec.tab[p] = (uint16_t)((c >> 8) | ((c & 0xFFu) << 8));
+    }
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    PhaseProf P;
+    P.init(nullptr);
+    const size_t remain = 6 + (size_t)len.x + len.y + len.z + len.w;
+    const bool ok = huf_decode1of4_wave64(tl, (const uint8_t*)hp, remain, (uint8_t*)dstp, rs, len.x | (len.y << 16), len.z,
+                                          wid, (lds_u32*)&stgAll[wid * kCoopStgWords + 2 * 64], P);
+    if (!ok && lane_id() == 0) atomicOr(&bad, 1u);
+    __syncthreads();
+    if (tid == 0 && bad) gst<int32_t>(&a.units[g * kStreams + (size_t)s].dres, (int32_t)z1::kDecErrHufStream);
+}
+
 // Small batches (the per-chunk calls): one workgroup of kCoopWaves waves per work unit.  Wave 0
 // decodes the frame; the four Huffman streams of each literals section are decoded by the four
 // waves at once, 64 lanes per stream (pgn_zdec.h CoopCmd).  A lone 100,000-sample chunk's decode
@@ -1898,6 +1946,8 @@ struct pgn_ctx {
     size_t deferTailPlain = 0;
     size_t deferHead = 0;      // PGN_DEFER_HEAD: chunks of a short first deferred pass (0 = balanced passes)
     bool hufPrioLast = false;  // PGN_HUF_PRIO_LAST=1: the last deferred pass's dec_huf waves at raised priority
+    bool lastOnCaller = false;  // PGN_LAST_ON_CALLER=1: the last deferred pass's sections and merge on the caller's stream
+    size_t hufWideLast = 0;    // PGN_HUF_WIDE_LAST: the last this many deferred passes decode their sections with dec_huf_wide_kernel
     bool lastDeferred = false;  // the last staged C5 decode deferred its Huffman sections (pgn_ctx_kernels)
     // encode: per-slot scratch of the zstd kernel, per-chunk streams/frames of one sub-batch
     uint8_t* encScratch = nullptr;
@@ -2070,6 +2120,8 @@ int pgn_ctx_create(int device, pgn_ctx** out)
     if (const char* v = getenv("PGN_DEFER_MIN_CHUNKS")) { const long x = atol(v); if (x > 0) c->deferMin = (size_t)x; }
     if (const char* v = getenv("PGN_DEFER_G")) { const long x = atol(v); if (x > 0) c->deferG = (size_t)x; }
     if (const char* v = getenv("PGN_DEFER_HEAD")) { const long x = atol(v); if (x >= 0) c->deferHead = (size_t)x; }
+    if (const char* v = getenv("PGN_LAST_ON_CALLER")) c->lastOnCaller = v[0] == '1';
+    if (const char* v = getenv("PGN_HUF_WIDE_LAST")) { const long x = atol(v); if (x >= 0) c->hufWideLast = (size_t)x; }
     if (const char* v = getenv("PGN_HUF_PRIO_LAST")) c->hufPrioLast = v[0] == '1';
     if (const char* v = getenv("PGN_DEFER_TAIL_PLAIN")) { const long x = atol(v); if (x >= 0) c->deferTailPlain = (size_t)x; }
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -2515,6 +2567,8 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         }
     }
     const size_t passes = pBase.size();
+    size_t nDefPasses = 0;  // deferred passes (an in-place tail pass comes last)
+    for (size_t p = 0; p < passes; p++) nDefPasses += defer && !pPlain[p] ? 1 : 0;
     const uint32_t nu = codec == kCodecVbz ? 1u : (uint32_t)kStreams;
     const size_t slots = nu * G < c->decSlotsMax ? nu * G : c->decSlotsMax;
     // few chunks: a workgroup per frame (not for the passes of a larger deferred call)
@@ -2595,19 +2649,27 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
             hipLaunchKernelGGL(dec_zstd_coop_kernel, dim3((unsigned)(nu * G)), dim3(64 * kCoopWaves), 0, s, a);
         else hipLaunchKernelGGL(dec_zstd_kernel, dim3((unsigned)slots), dim3(64), 0, s, a);
         // the stream of this pass's sections (deferred) or merge (otherwise)
-        const hipStream_t hs = multi ? (defer ? hufS[p % hufStreams] : c->side) : sideS;
-        if (multi) {
+        // (the last pass's on the caller's stream, right behind its frame decode: on side stream p % 3
+        // they would queue behind pass p - 3's merge, which ends ~1 ms after the frame decode,
+        // profiles/r06_decode_timeline_a.txt)
+        const bool lastOnCaller = defer && c->lastOnCaller && p + 1 == passes;
+        const hipStream_t hs = multi ? (defer ? (lastOnCaller ? s : hufS[p % hufStreams]) : c->side) : sideS;
+        if (multi && hs != s) {
             HIPCHK(hipEventRecord(c->evDStage[b], s));
             HIPCHK(hipStreamWaitEvent(hs, c->evDStage[b], 0));
         }
         // the deferred sections (kHufFrames frames of one stream type per wave), ahead of the pass's
         // merge: they overlap the next pass's frame decode
-        if (deferP)
+        // the last hufWideLast deferred passes: the latency-first decoder (dec_huf_wide_kernel)
+        const bool wide = deferP && p + c->hufWideLast >= nDefPasses;
+        if (deferP && wide)
+            hipLaunchKernelGGL(dec_huf_wide_kernel, dim3((unsigned)(nu * a.G)), dim3(64 * kCoopWaves), 0, hs, a);
+        else if (deferP)
             hipLaunchKernelGGL(dec_huf_kernel, dim3((unsigned)(nu * ((a.G + kHufFrames - 1) / kHufFrames))), dim3(64), 0, hs, a);
         // with deferred sections over several passes the merge goes to the third stream behind its
         // pass's sections (so it overlaps the next pass's sections); the buffer is free after it
         hipStream_t ms = hs;
-        if (defer && multi && hufStreams < 3) {
+        if (defer && multi && hufStreams < 3 && hs != s) {
             HIPCHK(hipEventRecord(c->evDHuf[b], hs));
             HIPCHK(hipStreamWaitEvent(c->mergeS, c->evDHuf[b], 0));
             ms = c->mergeS;

@@ -19,21 +19,23 @@ import _oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=[0, 40], ids=["all_deferred", "plain_tail"])
+@pytest.fixture(scope="module", params=[(0, 0), (40, 0), (0, 1000)], ids=["all_deferred", "plain_tail", "wide"])
 def dcodec(request):
     """Passes of 96 chunks; with plain_tail the last 40 chunks of a call are one pass whose Huffman
-    sections dec_zstd_kernel decodes in place (PGN_DEFER_TAIL_PLAIN)."""
+    sections dec_zstd_kernel decodes in place (PGN_DEFER_TAIL_PLAIN); with wide every pass's sections
+    go to the latency-first dec_huf_wide_kernel (PGN_HUF_WIDE_LAST)."""
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from rawnanoporesignalcompression_amd import PGNanoCodec
 
-    keys = ("PGN_DEFER_MIN_CHUNKS", "PGN_DEFER_G", "PGN_DEFER_TAIL_PLAIN")
+    keys = ("PGN_DEFER_MIN_CHUNKS", "PGN_DEFER_G", "PGN_DEFER_TAIL_PLAIN", "PGN_HUF_WIDE_LAST")
     old = {k: os.environ.get(k) for k in keys}
     os.environ["PGN_DEFER_MIN_CHUNKS"] = "1"
     os.environ["PGN_DEFER_G"] = "96"
-    os.environ["PGN_DEFER_TAIL_PLAIN"] = str(request.param)
+    os.environ["PGN_DEFER_TAIL_PLAIN"] = str(request.param[0])
+    os.environ["PGN_HUF_WIDE_LAST"] = str(request.param[1])
     try:
         c = PGNanoCodec(0)
     finally:

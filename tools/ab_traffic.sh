@@ -1,5 +1,5 @@
 #!/bin/bash
-# HBM traffic of the encode kernel per library build under ab/*.so (run via gpurun): the PGN_AB_SKIP
+# HBM traffic of the encode kernel per library build _ab/lib$n.so, n in LIBS (run via gpurun): the PGN_AB_SKIP
 # diagnostic builds stop the zstd stage after successive phases (1: no zstd stage, raw blocks; 2: match
 # search, then raw blocks; 3: + literal gather and histograms, raw literals; 4: + Huffman tables, no bit
 # packing; 0: the product), so the differences attribute enc_chunk_kernel's bytes to its phases.
@@ -7,10 +7,10 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/abt
 R=${1:-20000}
-for v in ab/*.so; do
-  n=$(basename $v .so)
+for n in ${LIBS:-A B}; do
+  v=_ab/lib$n.so
   for C in FETCH_SIZE WRITE_SIZE; do
-    PGN_LIB=$PWD/$v timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C --output-format csv \
+    PGN_ENCODE_ONLY=1 PGN_LIB=$PWD/$v timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C --output-format csv \
         -d gpurun_out/abt/${n}_$C -o run -- python3 tools/traffic_probe.py $R 100000 \
         > gpurun_out/abt/${n}_$C.log 2>&1 || { echo "$n $C failed"; tail -5 gpurun_out/abt/${n}_$C.log; exit 1; }
   done
