@@ -45,7 +45,7 @@ PORES = {"default": 6554, "r941": 7282, "r103": 6554, "r1041": 5243}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # PMC traffic summaries (tools/traffic.sh) per workload, read into roofline.traffic when their
 # source digest matches the kernels being run
-TRAFFIC_FILES = {"configs[1]": "traffic_r05.json", "configs[4]": "traffic_r05_config4.json"}
+TRAFFIC_FILES = {"configs[1]": "traffic_r06.json", "configs[4]": "traffic_r06_config4.json"}
 
 
 def parse(argv=None):

@@ -62,7 +62,9 @@ int pgn_pod5_compress_reads(pgn_pod5_batch *batch, uint32_t read_count, const in
 /* A record batch of signal rows (signal_table_reader.cpp:294-318): row i = data[offsets[i] ..
  * offsets[i + 1]) decodes to samples[i] samples, written back to back into out (room for the sum
  * of samples[]).  row_status (optional, row_count entries) receives each row's pgn_status; the
- * call returns the first non-zero row status, else PGN_OK. */
+ * call returns the first non-zero row status, else PGN_OK.  A row whose frames claim more content
+ * than the batch's intermediates hold is decoded again by the per-chunk call (its frames into exactly
+ * their claims, as the reference decodes them), so its status is the reference's. */
 int pgn_pod5_decompress_rows(pgn_pod5_batch *batch, uint32_t row_count, const uint64_t *offsets, const uint8_t *data,
                              const uint32_t *samples, int16_t *out, int32_t *row_status);
 

@@ -583,8 +583,19 @@ int pgn_pod5_decompress_rows(pgn_pod5_batch* b, uint32_t row_count, const uint64
         b->pool->run(&job, 1);
         const int32_t* st = (const int32_t*)(b->hRes[s].p + up256(maxOut));
         for (size_t i = 0; i < m; i++) {
-            if (row_status) row_status[r0 + i] = st[i];
-            if (first == PGN_OK && st[i] != PGN_OK) first = st[i];
+            int32_t sti = st[i];
+            if (sti == PGN_ERR_UNSUPPORTED && samples[r0 + i] <= PGN_MAX_CHUNK_SAMPLES) {
+                // frames claiming more than the batch's intermediates hold (the bounded call cannot list
+                // them without a host wait): the per-chunk call decodes the row as the reference does
+                const size_t r = r0 + i;
+                const uint8_t* src = data + offsets[r];
+                const size_t len = offsets[r + 1] - offsets[r];
+                sti = b->codec == PGN_POD5_CODEC_VBZ
+                          ? pgn_vbz_decompress_signal(b->ctx, src, len, out + sampleStart[r], samples[r])
+                          : pgn_variant_decompress_signal(b->ctx, b->codec, src, len, out + sampleStart[r], samples[r]);
+            }
+            if (row_status) row_status[r0 + i] = sti;
+            if (first == PGN_OK && sti != PGN_OK) first = sti;
         }
         return PGN_OK;
     };

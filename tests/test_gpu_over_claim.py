@@ -221,3 +221,28 @@ def test_claims_wrapping_64_bits_are_alloc(codecs):
     for codec in (plain, deferred):
         _, st = _decode_batch(codec, [blob] * 3 + [O.c5_compress(x)[1]] * 67, [x.size] * 70)
         assert st.tolist() == [8] * 3 + [0] * 67
+
+
+@pytest.mark.gpu
+def test_over_claim_status_in_pod5_rows(codecs):
+    """The batched POD5 row decode (include/pgnano_pod5.h, bounded by the rows' sample counts): a row
+    whose frames expand past the batch's intermediates gets the reference's status too."""
+    from rawnanoporesignalcompression_amd import PGNanoError, Pod5SignalBatch
+
+    plain, _ = codecs
+    x, cases = _cases()
+    ok_blob = O.c5_compress(x)[1]
+    for k in ("lhigh_expands_300k", "m_and_lhigh_expand"):
+        blobs = [ok_blob] * 5 + [cases[k][0]] + [ok_blob] * 3
+        offsets = np.concatenate([[0], np.cumsum([len(b) for b in blobs])]).astype(np.uint64)
+        data = np.frombuffer(b"".join(blobs), np.uint8)
+        samples = np.full(len(blobs), x.size, np.uint32)
+        b = Pod5SignalBatch(plain)
+        try:
+            with pytest.raises(PGNanoError) as ei:
+                b.decompress_rows(offsets, data, samples)
+            assert ei.value.status == EXPECT[k]
+            good = b.decompress_rows(offsets[:6], data[: int(offsets[5])], samples[:5])
+            assert np.array_equal(good, np.tile(x, 5))
+        finally:
+            b.close()

@@ -1,15 +1,17 @@
 #!/bin/bash
-# Round-5 evidence of the committed sources: HBM traffic of configs[1] and configs[4] first (so the
-# bench lines below carry roofline.traffic for these kernels), GPU tests, smoke, default bench, kernel
-# trace of the default bench and its decode timeline, configs[4] decode bench; with EXTRA=1 also the
-# configs[2] (R10.4.1, VBZ ratio) and configs[3] (1,000,000 distinct reads) lines and the --gpus 2
-# launcher rehearsed with two gloo ranks on the box's one GPU.
-TAG=${1:-r05}
+# Evidence of the committed sources (run via gpurun): HBM traffic of configs[1] and configs[4] first
+# (copied to profiles/traffic_$ROUND.json and traffic_${ROUND}_config4.json, which bench.py reads into
+# roofline.traffic when their source digest matches), GPU tests, smoke, default bench, kernel trace of
+# the default bench and its decode timeline, configs[4] decode bench; with EXTRA=1 also the configs[2]
+# (R10.4.1, VBZ ratio) and configs[3] (1,000,000 distinct reads) lines and the --gpus 2 launcher
+# rehearsed with two gloo ranks on the box's one GPU.   ROUND=r06 bash tools/gpu_final.sh TAG
+TAG=${1:-final}
+ROUND=${ROUND:-r06}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-bash tools/traffic.sh $TAG && cp gpurun_out/traffic_$TAG.json profiles/traffic_r05.json \
+bash tools/traffic.sh $TAG && cp gpurun_out/traffic_$TAG.json profiles/traffic_$ROUND.json \
 && bash tools/traffic.sh ${TAG}_config4 100000 100000 mixed \
-&& cp gpurun_out/traffic_${TAG}_config4.json profiles/traffic_r05_config4.json \
+&& cp gpurun_out/traffic_${TAG}_config4.json profiles/traffic_${ROUND}_config4.json \
 && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > gpurun_out/gpu_tests_$TAG.log 2>&1 \
 && timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
