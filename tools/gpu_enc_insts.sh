@@ -7,7 +7,7 @@ O=gpurun_out/${1:-encinsts}
 mkdir -p $O
 R=20000
 for n in $LIBS; do
-  PGN_ENCODE_ONLY=1 PGN_LIB=$PWD/_ab/lib$n.so timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES \
+  PGN_ENCODE_ONLY=1 PGN_LIB=$PWD/_ab/lib$n.so timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS \
       --output-format csv -d $O/$n -o run -- python3 tools/phase_profile.py $R > $O/$n.log 2>&1 || { echo "$n failed"; tail -5 $O/$n.log; exit 1; }
   python3 - "$O/$n" "$n" "$R" <<'PY'
 import csv, glob, sys, collections
@@ -20,6 +20,7 @@ for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
 for k in sorted(agg):
     v = agg[k]
     if k.startswith("enc_") and v["SQ_INSTS_VALU"] > 1e6:
-        print(f"{n} {k}: VALU {v['SQ_INSTS_VALU']/R/1e3:.1f}k SALU {v['SQ_INSTS_SALU']/R/1e3:.1f}k LDS {v['SQ_INSTS_LDS']/R/1e3:.1f}k per chunk")
+        print(f"{n} {k}: VALU {v['SQ_INSTS_VALU']/R/1e3:.1f}k SALU {v['SQ_INSTS_SALU']/R/1e3:.1f}k LDS {v['SQ_INSTS_LDS']/R/1e3:.1f}k "
+              f"LDS bank-conflict cycles {v['SQ_LDS_BANK_CONFLICT']/R/1e3:.1f}k active LDS cycles {v['SQ_ACTIVE_INST_LDS']/R/1e3:.1f}k per chunk")
 PY
 done
