@@ -23,8 +23,8 @@ constexpr uint32_t kJobTabUse = 352;  // entries a job's compact table may have:
 constexpr unsigned kHufLdsLog = 11;  // Huffman tables up to this log live in LDS (zstd's encoders
                                      // never exceed 11); a 12-bit table is built in HBM (slow path)
 
-// The Huffman table build's LDS (huf_build_dtable_body): part of DecLds in the frame decoder, a
-// __shared__ of its own (1 KiB) in dec_zfast_kernel, which builds only jobs' compact tables.
+// The Huffman table build's LDS (huf_build_dtable_body): part of DecLds (sDec.hb), used by the frame
+// decoder and by dec_frame_fast's job-only build in dec_zstd_kernel.
 struct HufBuildLds {
     uint8_t wts[256];         // weights of the current table
     uint8_t order[256];       // symbols sorted by (weight, symbol)
