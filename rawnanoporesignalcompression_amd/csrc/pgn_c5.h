@@ -29,7 +29,6 @@ struct C5Streams {
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kSplitStep = 1024;
 constexpr uint32_t kWinBytes = 1088;  // 31 carried nibbles + 1024 new, rounded up to 16
-constexpr uint32_t kDummy = kWinBytes;  // + 4 * lane: per-lane discard slots (distinct banks)
 
 struct SplitLds {
     alignas(16) uint8_t S[kWinBytes + 256];  // one byte per nibble
@@ -37,6 +36,7 @@ struct SplitLds {
     alignas(16) uint8_t L[kWinBytes];
     alignas(16) uint8_t H[kWinBytes];
     alignas(16) uint32_t Z[64 * 8];  // a lane's 16 zig-zag values (two per word), for its class-3 samples
+    alignas(16) uint8_t D[64 * 16];  // a lane's 16 discard bytes (what its class-0 / class-3 samples write)
 };
 
 typedef uint16_t pgn_u16x2 __attribute__((ext_vector_type(2)));
@@ -196,16 +196,22 @@ __device__ __forceinline__ uint32_t split_step(const uint4& a, const uint4& b, c
     uint8_t* const wb = reinterpret_cast<uint8_t*>(&W);
     constexpr uint32_t offS = (uint32_t)__builtin_offsetof(SplitLds, S), offM = (uint32_t)__builtin_offsetof(SplitLds, M);
     const uint32_t baseS = offS + fS + (exc & 0x7FFu), baseM = offM + fM + ((exc >> 11) & 0x7FFu);
-    const uint32_t dS = offS + kDummy + 4u * lane;  // classes 0 and 3: a per-lane discard slot
+    // the lane's four next places as the 16-bit fields of one 64-bit word, field c = class c (classes
+    // 0 and 3 write the lane's discard bytes): sample m's place is field c_m (one v_perm_b32), and
+    // that field advances by one byte (1 << 16 c_m)
+    constexpr uint32_t offD = (uint32_t)__builtin_offsetof(SplitLds, D);
+    static_assert(sizeof(SplitLds) < 65536, "split places are 16-bit");
+    const uint32_t dD = offD + 16u * lane;
+    uint32_t plo = dD | (baseS << 16), phi = baseM | (dD << 16);
 #pragma unroll
     for (int m = 0; m < 16; m++) {
-        // class 1: S window at its rank among the lane's class-1 samples; class 2: M likewise;
-        // classes 0 and 3: the discard slot (empty mask, rank 0)
-        const uint32_t below = (1u << (2 * m)) - 1u;
-        const uint32_t bS = (uint32_t)__builtin_amdgcn_sbfe((int)m1, 2 * m, 1), bM = (uint32_t)__builtin_amdgcn_sbfe((int)m2, 2 * m, 1);
-        const uint32_t msk = bfi32(bS, m1, m2 & bM);
-        const uint32_t base = bfi32(bS, baseS, bfi32(bM, baseM, dS));
-        const uint32_t at = base + (uint32_t)__builtin_popcount(msk & below);
+        const uint32_t c = __builtin_amdgcn_ubfe(kw, 2 * m, 2);
+        const uint32_t at = __builtin_amdgcn_perm(phi, plo, c * 0x0202u + 0x0C0C0100u);
+        if (m < 15) {
+            const uint64_t inc = (uint64_t)1 << (16 * c);
+            plo += (uint32_t)inc;
+            phi += (uint32_t)(inc >> 32);
+        }
         wb[at] = (uint8_t)(val[m >> 1] >> (16 * (m & 1)));
     }
     // field 3 has 10 bits: a step of 1024 class-3 samples wraps the inclusive total (the exclusive
@@ -459,10 +465,12 @@ struct MergeLds {
     // to back: S (one nibble per entry) from a 16-byte aligned stream byte, then M likewise, then L | H << 8.
     // A step has at most 1024 of them together, plus the alignment slack of two windows.
     alignas(16) uint16_t V[1024 + 64 + 32 + 32];
-    uint16_t zero[2];  // what a class-0 sample reads
+    uint16_t zero[16];  // what class-0 samples read (a lane's place here advances with them)
     // S byte -> its two entries (low nibble first), offset added and zig-zag decoded
     alignas(16) uint32_t nib[256];
 };
+
+static_assert(sizeof(MergeLds) < 65536, "merge places are 16-bit");
 
 // stage bytes [a, a + len) of `in` (len <= cap - 15) into W; returns the window's first address
 __device__ __forceinline__ uint64_t stage_bytes(uint8_t* W, const uint8_t* in, uint64_t a, uint32_t len)
@@ -496,40 +504,43 @@ __device__ __forceinline__ void put_bytes16(uint16_t* d, const uint4& v, uint32_
 
 // Merge step over 1024 samples: lane l decodes the 16 consecutive samples t + 16l .. t + 16l + 15,
 // whose 16 keys are its own key word.  Every class has a staged 16-bit window of deltas (offsets
-// added and zig-zag decoded at staging; class 0 reads a zero), and the lane's first place in each is
-// the step's fill plus the class counts of the lanes below it (one packed DPP scan).  Sample m's
-// place is its class's first place plus twice the number of earlier samples of its class in the key
-// word: one popcount of the class's pair mask below m (both bits of a pair set, so the count comes
-// out doubled = the entry's byte stride), the mask and the first place picked by a two-level bit
-// select on the sample's two key bits.  So a sample is one LDS read and a running 16-bit sum, and a
-// second scan carries the sum across lanes.  Outputs leave as two 16-byte stores per lane.
+// added and zig-zag decoded at staging; class 0 reads zeros), and the lane's first place in each is
+// the step's fill plus the class counts of the lanes below it (one packed DPP scan).  The lane keeps
+// its four next places as the 16-bit fields of one 64-bit word, field c = class c: sample m's place
+// is field c_m (one v_perm_b32 whose selector is c_m * 0x0202 + 0x0C0C0100), and the field advances
+// by one entry (2 << 16 c_m, a 64-bit shift and add).  So a sample is four ALU ops to its place, one
+// LDS read and a running 16-bit sum, and a second scan carries the sum across lanes.  Outputs leave
+// as two 16-byte stores per lane.
 __device__ __forceinline__ void merge_step(const MergeLds& W, uint32_t kw, uint32_t pS, uint32_t pM, uint32_t pL,
                                            uint32_t& carry, int16_t* __restrict__ out, uint32_t t, uint32_t n, bool full)
 {
     const uint32_t lane = (uint32_t)lane_id();
     const uint8_t* wb = reinterpret_cast<const uint8_t*>(&W);
     constexpr uint32_t pZ = (uint32_t)__builtin_offsetof(MergeLds, zero);
-    const uint32_t klo = kw & 0x55555555u, khi = (kw >> 1) & 0x55555555u;
-    const uint32_t dS = (klo & ~khi) * 3u, dM = (khi & ~klo) * 3u, dL = (klo & khi) * 3u;
-    uint32_t acc = 0;
-    uint32_t w[8];  // running sums, two 16-bit samples per word
+    // places are below sizeof(MergeLds) < 2^16
+    uint32_t plo = pZ | (pS << 16), phi = pM | (pL << 16);
+    uint32_t acc = 0;  // the running sum (its low 16 bits)
+    uint32_t w[8];     // running sums, two 16-bit samples per word
 #pragma unroll
-    for (int m = 0; m < 16; m++) {
-        // the class bits as all-ones / all-zero masks (v_bfe_i32), the place and the rank mask picked
-        // by v_bfi_b32 (asm: written as and/or, the selects became compare + cndmask pairs)
-        const uint32_t b0 = (uint32_t)__builtin_amdgcn_sbfe((int)kw, 2 * m, 1);
-        const uint32_t b1 = (uint32_t)__builtin_amdgcn_sbfe((int)kw, 2 * m + 1, 1);
-        uint32_t at = bfi32(b1, bfi32(b0, pL, pM), bfi32(b0, pS, pZ));
-        if (m > 0) {
-            const uint32_t d = bfi32(b1, bfi32(b0, dL, dM), dS & b0) & ((1u << (2 * m)) - 1u);
-            at += (uint32_t)__builtin_popcount(d);
+    for (int k = 0; k < 8; k++) {
+        uint32_t a[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int m = 2 * k + h;
+            const uint32_t c = __builtin_amdgcn_ubfe(kw, 2 * m, 2);
+            const uint32_t at = __builtin_amdgcn_perm(phi, plo, c * 0x0202u + 0x0C0C0100u);
+            if (m < 15) {
+                const uint64_t inc = (uint64_t)2 << (16 * c);
+                plo += (uint32_t)inc;
+                phi += (uint32_t)(inc >> 32);
+            }
+            acc += *reinterpret_cast<const uint16_t*>(wb + at);
+            a[h] = acc;
         }
-        const uint32_t v = *reinterpret_cast<const uint16_t*>(wb + at);
-        acc += v;
-        if (m & 1) w[m >> 1] |= acc << 16;
-        else w[m >> 1] = acc & 0xFFFFu;
-        if (m % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // at most 4 places read ahead (VGPRs)
+        w[k] = __builtin_amdgcn_perm(a[1], a[0], 0x05040100u);  // the two sums' low halves
+        if (k & 1) __builtin_amdgcn_sched_barrier(0);  // at most 4 places read ahead (VGPRs)
     }
+    acc &= 0xFFFFu;
     const uint32_t incl = wave_incl_sum(acc);
     const uint32_t base = carry + incl - acc;
     carry += readlane_u32(incl, 63);
@@ -596,7 +607,7 @@ __device__ __forceinline__ int c5_merge_range(const uint8_t* __restrict__ in, ui
     const uint32_t kl = (n + 3) / 4;
     const uint32_t ps = kl, pm = kl + (uint32_t)dS, pl = pm + (uint32_t)dM, ph = pl + (uint32_t)dLl;
     uint32_t sN = (uint32_t)sN0, mN = (uint32_t)mN0, lN = (uint32_t)lN0;  // before the next step to plan (wave-uniform)
-    if (lane == 0) W.zero[0] = 0;
+    if (lane < 16) W.zero[lane] = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {  // the S table: byte -> two entries
         const uint32_t bt = 4 * lane + q;
