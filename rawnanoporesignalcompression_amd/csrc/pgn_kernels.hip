@@ -2602,7 +2602,7 @@ static int launch_decode_impl(pgn_ctx* c, int codec, size_t nchunks, const uint8
         HIPCHK(hipEventRecord(c->evFork, s));
         HIPCHK(hipStreamWaitEvent(c->side, c->evFork, 0));
     }
-    DecArgs a;
+    DecArgs a{};
     a.nchunks = nchunks;
     a.in = d_in;
     a.inOffsets = d_in_offsets;
